@@ -1,0 +1,129 @@
+// hc_cli.cpp — `huffman-codec`, the drop-in command line of the MI355X codec.
+//
+// Same contract as the reference's src/main.cpp:152-221: getopt(":cdmai:o:w:h"), -c default,
+// last of -c/-d wins, -w parsed by std::stoull (default 512; a non-numeric value throws and
+// aborts exactly like the reference), -o default b.out, the same help text, error messages and
+// exit codes 1-15, and the stderr line "writing N bytes to F". Compression and decompression
+// run on the GPU through include/hcodec.h.
+#include <unistd.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+#include "hcodec.h"
+
+namespace {
+
+const char *const kHelp =
+    "USAGE:\n"
+    "  huffman-codec [-cm] -i IFILE [-o OFILE]\n"
+    "  huffman-codec [-cm] -a [-w WIDTH] -i IFILE [-o OFILE]\n"
+    "  huffman-codec -d -i IFILE [-o OFILE] | -h\n"
+    "\n"
+    "OPTION:\n"
+    "  -c/-d  perform compression/decompression\n"
+    "  -m     use differential model for preprocessing\n"
+    "  -a     use adaptive block RLE (default: RLE)\n"
+    "  -w     width of 2D data (default: 512)\n"
+    "  -i     input file path\n"
+    "  -o     output file path (default: b.out)\n"
+    "  -h     show this help\n";
+
+void error_hint(const char *msg)  // main.cpp:147-149
+{
+    std::cerr << msg << "try 'huffman-codec -h' for more information\n";
+}
+
+// the reference's messages for the statuses its library exits with
+const char *status_message(int st)
+{
+    switch (st) {
+    case HC_ERR_MATRIX_SIZE: return "ERROR: invalid size of input 2D data detected\n";
+    case HC_ERR_HEADER: return "ERROR: invalid or missing Huffman coding header\n";
+    case HC_ERR_HUFFMAN: return "ERROR: invalid Huffman coding file contents\n";
+    case HC_ERR_ADAPT_HEADER: return "ERROR: invalid or missing adaptive block RLE header\n";
+    case HC_ERR_ADAPT_DIRS: return "ERROR: invalid adaptive block RLE header\n";
+    case HC_ERR_DIMS: return "ERROR: too small 2D data dimensions\n";
+    case HC_ERR_BLOCK_DATA: return "ERROR: invalid adaptive block RLE file contents\n";
+    case HC_ERR_BLOCK_EOF: return "ERROR: unexpected end of adaptive block RLE data\n";
+    case HC_ERR_LEFTOVER: return "ERROR: leftover data of adaptive block RLE detected\n";
+    case HC_ERR_BLOCK_SIZE: return "ERROR: invalid adaptive block RLE block size\n";
+    case HC_ERR_TOO_LARGE: return "ERROR: adaptive block RLE matrix too large\n";
+    case HC_ERR_UNSUPPORTED: return "ERROR: stream exceeds the device coder's limits\n";
+    case HC_ERR_DEVICE: return "ERROR: no usable gfx950 GPU (HIP runtime error)\n";
+    default: return "ERROR: codec failure\n";
+    }
+}
+
+}  // namespace
+
+int main(int argc, char *argv[])
+{
+    bool compress = true, use_diff = false, use_adapt = false;
+    std::string ifp, ofp = "b.out";
+    uint64_t width = 512;
+
+    int opt;
+    while ((opt = getopt(argc, argv, ":cdmai:o:w:h")) != -1) {
+        switch (opt) {
+        case 'c': compress = true; break;
+        case 'd': compress = false; break;
+        case 'm': use_diff = true; break;
+        case 'a': use_adapt = true; break;
+        case 'i': ifp = optarg; break;
+        case 'o': ofp = optarg; break;
+        case 'w': width = std::stoull(optarg); break;  // throws like main.cpp:176
+        case 'h': std::cout << kHelp; return 0;
+        case ':': error_hint("ERROR: missing additional argument\n"); return 1;
+        case '?': error_hint("ERROR: unrecognized option used\n"); return 2;
+        }
+    }
+    if (ifp.empty()) {
+        error_hint("ERROR: no input file path provided\n");
+        return 3;
+    }
+    if (compress && width == 0) {
+        error_hint("ERROR: invalid 2D data width\n");
+        return 4;
+    }
+    std::ifstream ifs(ifp, std::ios::in | std::ios::binary);
+    if (ifs.fail()) {
+        std::cerr << "ERROR: given input file does not exist\n";
+        return 5;
+    }
+    const std::vector<uint8_t> in((std::istreambuf_iterator<char>(ifs)), std::istreambuf_iterator<char>());
+    ifs.close();
+
+    std::vector<uint8_t> out;
+    int st;
+    if (compress) {
+        out.resize(hc_compress_bound(in.size(), use_adapt ? 1 : 0));
+        uint64_t len = 0;
+        st = hc_compress(in.data(), in.size(), use_diff, use_adapt, width, out.data(), out.size(), &len);
+        out.resize(st == HC_OK ? len : 0);
+    } else {
+        uint8_t *p = nullptr;
+        uint64_t len = 0;
+        st = hc_decompress_alloc(in.data(), in.size(), &p, &len);
+        if (st == HC_OK) out.assign(p, p + len);
+        hc_free(p);
+    }
+    if (st != HC_OK) {
+        std::cerr << status_message(st);
+        return st;
+    }
+
+    std::cerr << "writing " << out.size() << " bytes to " << ofp << "\n";  // main.cpp:218
+    std::ofstream ofs(ofp, std::ios::out | std::ios::binary);                // main.cpp:132-144
+    if (ofs.fail()) {
+        std::cerr << "ERROR: cannot write to " << ofp << " output file\n";
+        return 7;
+    }
+    ofs.write(reinterpret_cast<const char *>(out.data()), (std::streamsize)out.size());
+    return 0;
+}

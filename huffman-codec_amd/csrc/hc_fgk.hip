@@ -1,0 +1,623 @@
+// hc_fgk.hip — FGK adaptive-Huffman encode / decode for gfx950, one stream per wavefront.
+//
+// Reference: huffman.cpp:23-217 (HuffTree), transform.cpp:363-406 (applyHuffman /
+// revertHuffman), fused with transform.cpp:220-292 (diff model, MNP-5 RLE and their inverses)
+// and the header / bit packing of headers.cpp:107-125 and main.cpp:39-128.
+//
+// Design:
+//  * The FGK stream is serial, so parallelism comes from the batch: each 64-lane wavefront owns
+//    one stream, four wavefronts per 256-thread workgroup, 8 workgroups (32 waves) per CU.
+//  * The tree lives in LDS in the implicit slot form of SURVEY.md Appendix A.5: position p in
+//    0..512 carries the reference's node number p (root = 512), siblings are (2k, 2k+1), code
+//    bit = p & 1, weights non-decreasing in p. Per position one packed word
+//    weight << 10 | parent ("narrow", <= 2^22-2 symbols) or a 32-bit weight plus a separate
+//    parent array ("wide").
+//  * Per update level ONE lane-parallel LDS read fetches the words of positions s..s+63; a
+//    64-bit ballot of "weight == w[s]" is a prefix mask (weights sorted), so its trailing-ones
+//    count gives the block leader of huffman.cpp:157-184 (highest number with equal weight)
+//    in one step.
+//  * All control state (positions, bit accumulators, run-length FSM) is wave-uniform and lives
+//    in SGPRs. To keep the compiler from turning it into exec-masked VGPR code, the hot loops
+//    contain NO lane-divergent control flow: a store "from lane 0 only" is an all-lane store
+//    whose other lanes land in a per-wave scratch row, and global memory goes through buffer
+//    descriptors whose hardware range check replaces per-lane bounds tests.
+//  * Output bits gather in a 64-bit scalar accumulator, flush as big-endian dwords into a VGPR
+//    stage and leave as one coalesced 256-byte buffer store per 64 words.
+#include "hc_internal.h"
+
+namespace hc {
+namespace {
+
+constexpr uint32_t kRoot = 512;
+constexpr uint32_t kWords = 516;  // positions 0..512 + sentinels 513..515
+constexpr uint32_t kInner = 0x100;
+constexpr uint32_t kNyt = 0x200;
+constexpr int kWaves = 4;
+constexpr uint32_t kMaxBufBytes = 0x7FFFFF00u;  // per-stream limit of the 32-bit buffer offsets
+constexpr uint32_t kDrop = 0x7FFFFFF8u;         // buffer offset past every range: access dropped
+
+template <bool kWide>
+struct alignas(16) Tree {
+    uint32_t wt[kWords];              // narrow: weight << 10 | parent; wide: weight
+    uint32_t scratch[64];             // landing words of lanes that must not write
+    uint16_t body[kWords];            // symbol | kInner + child pair | kNyt
+    uint16_t where[256];              // symbol -> position, 0 = not yet transmitted
+    uint16_t up[kWide ? kWords : 8];  // wide: parent position
+};
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x)
+{
+    return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
+}
+__device__ __forceinline__ uint32_t lane_id()
+{
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// range-checked view of one stream's bytes; the arguments must be wave-uniform
+__device__ __forceinline__ rsrc_t make_rsrc(const uint8_t *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t buf_load(rsrc_t r, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_store(rsrc_t r, uint32_t off, uint32_t v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_store8(rsrc_t r, uint32_t off, uint32_t v)
+{
+    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, r, (int)off, 0, 0);
+}
+
+// ------------------------------------------------------------------------------ the tree --
+
+template <bool kWide>
+struct Fgk {
+    static constexpr uint32_t kInc = kWide ? 1u : 1024u;
+
+    Tree<kWide> &T;
+    uint32_t lane;
+    uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
+    uint32_t rootw;  // the root's word (weight = symbols coded so far)
+    uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
+
+    __device__ Fgk(Tree<kWide> &t, uint32_t l) : T(t), lane(l), nyt(kRoot), rootw(0), bad(0)
+    {
+        // huffman.cpp:23-31: a lone NYT root
+        for (uint32_t i = lane; i < kWords; i += 64) {
+            T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
+            T.body[i] = i == kRoot ? kNyt : 0;
+            if (kWide) T.up[i] = 0;
+        }
+        for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // own scratch slot of this lane (16- and 32-bit views)
+    __device__ __forceinline__ uint32_t *scr32() const { return &T.scratch[lane]; }
+    __device__ __forceinline__ uint16_t *scr16() const
+    {
+        return reinterpret_cast<uint16_t *>(&T.scratch[lane]);
+    }
+
+    // huffman.cpp:99-111: split NYT at t -> NYT at t-2 (left), symbol leaf at t-1 (right).
+    // Lanes 0..2 write the three bodies, lanes 0..1 the two parent links, lane 0 the map.
+    __device__ __forceinline__ uint32_t split(uint32_t sym)
+    {
+        const uint32_t t = nyt;
+        const uint32_t bpos = lane == 0 ? t : (lane == 1 ? t - 2 : t - 1);
+        const uint32_t bval = lane == 0 ? (kInner | ((t - 2) >> 1)) : (lane == 1 ? kNyt : sym);
+        *(lane < 3 ? &T.body[bpos] : scr16()) = (uint16_t)bval;
+        *(lane == 0 ? &T.where[sym] : scr16()) = (uint16_t)(t - 1);
+        if (kWide) *(lane < 2 ? &T.up[t - 2 + lane] : scr16()) = (uint16_t)t;
+        else *(lane < 2 ? &T.wt[t - 2 + lane] : scr32()) = t;  // weight 0, parent t
+        __builtin_amdgcn_wave_barrier();
+        nyt = t - 2;
+        return t - 1;
+    }
+
+    // huffman.cpp:186-217 in slot form: exchange the contents of positions s and l (their
+    // weights are equal), then re-point what hangs below them. Lane k < 2 writes the content
+    // moving into (k ? l : s); lane k < 4 re-parents child (k & 1) of content (k >> 1).
+    __device__ __forceinline__ void swap(uint32_t s, uint32_t l)
+    {
+        const uint32_t bs = uni(T.body[s]);
+        const uint32_t bl = uni(T.body[l]);
+        const uint32_t k = lane >> 1;                 // 0: content going to s, 1: to l
+        const uint32_t b = (lane & 1) ? bs : bl;      // lanes 0/1: body for s / l
+        const uint32_t pos = (lane & 1) ? l : s;
+        *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
+        *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
+        const uint32_t cb = k ? bs : bl;              // lanes 0..3: content whose child moves
+        const uint32_t cpos = k ? l : s;
+        const bool inner = lane < 4 && (cb & kInner);
+        const uint32_t c = (cb & 255u) * 2 + (lane & 1);
+        if (kWide) {
+            *(inner ? &T.up[c] : scr16()) = (uint16_t)cpos;
+        } else {
+            uint32_t *q = inner ? &T.wt[c] : scr32();
+            *q = (*q & ~1023u) | cpos;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // highest position >= from whose weight equals that of word w, when positions
+    // from-64..from-1 all had it
+    __device__ uint32_t leader_far(uint32_t from, uint32_t w)
+    {
+        const uint32_t lim = kWide ? w : (w | 1023u);
+        for (;;) {
+            const uint32_t a = min(from + lane, kWords - 1);
+            const uint64_t le = ballot(T.wt[a] <= lim);
+            if (le != ~0ull) return from + (uint32_t)__builtin_ctzll(~le) - 1;
+            from += 64;
+        }
+    }
+
+    // huffman.cpp:95-128 (update) from position s upward. With kRecord, also collects the
+    // PRE-update code of the path (huffman.cpp:136-155) into rev (bit i = level i above the
+    // leaf) for levels >= first; on the first swap the rest of the old path is read before
+    // the tree changes above it.
+    template <bool kRecord>
+    __device__ __forceinline__ void update(uint32_t s, uint32_t first, uint64_t &rev, uint32_t &d)
+    {
+        bool rec = kRecord;
+        uint32_t lvl = 0;
+        while (s != kRoot) {
+            const uint32_t a = min(s + lane, kWords - 1);
+            const uint32_t v = T.wt[a];
+            uint32_t ws = uni(v);
+            // positions >= s weigh >= w[s]; "same weight" = "word <= w[s] with all low bits"
+            const uint64_t le = ballot(v <= (kWide ? ws : (ws | 1023u)));
+            uint32_t p = kWide ? uni(T.up[s]) : (ws & 1023u);
+            if (kRecord && rec && lvl >= first) {
+                rev |= (uint64_t)(s & 1u) << d;
+                ++d;
+            }
+            const uint32_t lead = le != ~0ull ? s + (uint32_t)__builtin_ctzll(~le) - 1 : leader_far(s + 64, ws);
+            if (lead != s && lead != p) {
+                if (kRecord && rec) {  // finish the old code path first (read-only walk)
+                    for (uint32_t x = p; x != kRoot;) {
+                        rev |= (uint64_t)(x & 1u) << d;
+                        ++d;
+                        const uint32_t nx = kWide ? uni(T.up[x]) : (uni(T.wt[x]) & 1023u);
+                        if (nx <= x || d >= 64) {
+                            bad = 1;
+                            return;
+                        }
+                        x = nx;
+                    }
+                    rec = false;
+                }
+                swap(s, lead);
+                // the swap rewrites only the parent fields below s and lead, never their own
+                // words, so the pre-swap read still holds lead's word when it was in range
+                const uint32_t off = lead - s;
+                ws = off < 64 ? lane_read(v, off) : uni(T.wt[lead]);
+                s = lead;
+                p = kWide ? uni(T.up[s]) : (ws & 1023u);
+            }
+            *(lane == 0 ? &T.wt[s] : scr32()) = ws + kInc;
+            __builtin_amdgcn_wave_barrier();
+            if (p <= s) {  // parents sit above their children: anything else is corruption
+                bad = 1;
+                return;
+            }
+            s = p;
+            ++lvl;
+        }
+        rootw += kInc;
+        *(lane == 0 ? &T.wt[kRoot] : scr32()) = rootw;
+        __builtin_amdgcn_wave_barrier();
+    }
+};
+
+// ------------------------------------------------------------------------- output stage --
+
+// Bits gather in a scalar accumulator and leave as big-endian dwords through a VGPR stage of
+// 64 words (one coalesced 256-byte buffer store). The u64 count (words 0-1) is rewritten at
+// the end by the same lanes that first stored them, so program order keeps it last.
+struct BitSink {
+    rsrc_t rs;
+    uint32_t lane;
+    uint32_t wbase;  // word index of stage lane 0
+    uint32_t widx;   // next stage lane
+    uint32_t stage;
+    uint64_t acc;
+    uint32_t nacc;
+
+    __device__ __forceinline__ void word(uint32_t w)
+    {
+        stage = lane == widx ? __builtin_bswap32(w) : stage;
+        if (++widx == 64) {
+            buf_store(rs, (wbase + lane) * 4, stage);
+            wbase += 64;
+            widx = 0;
+        }
+    }
+    // append the n (<= 32) low bits of x, MSB first
+    __device__ __forceinline__ void put(uint32_t x, uint32_t n)
+    {
+        acc = (acc << n) | x;
+        nacc += n;
+        if (nacc >= 32) {
+            nacc -= 32;
+            word((uint32_t)(acc >> nacc));
+        }
+    }
+    __device__ __forceinline__ void put64(uint64_t x, uint32_t n)
+    {
+        if (n > 32) {
+            put((uint32_t)(x >> 32), n - 32);
+            put((uint32_t)x, 32);
+        } else {
+            put((uint32_t)x, n);
+        }
+    }
+    // zero-pad to a byte (transform.cpp:379-381); store what is left; return the byte length
+    __device__ __forceinline__ uint64_t finish()
+    {
+        if (nacc & 7u) put(0, 8 - (nacc & 7u));
+        const uint32_t tail = nacc >> 3;  // 0..3 bytes pending
+        const uint32_t tw = tail ? (uint32_t)(acc << (32 - nacc)) : 0u;  // MSB-aligned
+        // whole words of the stage, then the tail bytes from lane widx
+        buf_store(rs, lane < widx ? (wbase + lane) * 4 : kDrop, stage);
+        const uint32_t tb = (wbase + widx) * 4;
+        for (uint32_t b = 0; b < 3; ++b)
+            buf_store8(rs, lane == widx && b < tail ? tb + b : kDrop, tw >> (24 - 8 * b));
+        return (uint64_t)(wbase + widx) * 4 + tail;
+    }
+};
+
+// --------------------------------------------------------------------------- the encoder --
+
+template <bool kWide, int kSrc>
+__global__ __launch_bounds__(256) void encode_kernel(Batch bt)
+{
+    __shared__ Tree<kWide> trees[kWaves];
+    const uint32_t lane = lane_id();
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t sid = blockIdx.x * kWaves + wv;
+    if (sid >= bt.n) return;
+
+    const uint64_t in_off = uni64(bt.in_offs[sid]);
+    const uint64_t n = uni64(bt.in_lens[sid]);
+    const uint64_t out_off = uni64(bt.out_offs[sid]);
+    const uint64_t cap = uni64(bt.out_caps[sid]);
+
+    // worst-case symbol count decides narrow / wide; the other variant's launch skips
+    const uint64_t max_sym = kSrc == SRC_SYMBOLS ? n : n + n / 3 + 2;
+    const bool narrow_ok = max_sym <= kNarrowMaxSymbols;
+    if (kWide == narrow_ok) return;
+    if (max_sym > kWideMaxSymbols || n > kMaxBufBytes) {
+        if (lane == 0) {
+            bt.status[sid] = HC_ERR_UNSUPPORTED;
+            bt.out_lens[sid] = 0;
+        }
+        return;
+    }
+
+    Fgk<kWide> fgk(trees[wv], lane);
+    BitSink sink;
+    sink.rs = make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
+    sink.lane = lane;
+    sink.wbase = 0;
+    sink.widx = 2;  // words 0-1: the u64 symbol count, written again at the end
+    sink.stage = 0;
+    sink.acc = 0;
+    sink.nacc = 0;
+    const uint32_t flags = kSrc == SRC_SYMBOLS ? bt.flags : (kSrc == SRC_RAW_DIFF ? 0x80u : 0u);
+    sink.put(flags, 8);  // headers.cpp:118-122
+
+    uint64_t nsym = 0;
+    const uint32_t n32 = (uint32_t)n;
+    const rsrc_t rin = make_rsrc(bt.in + in_off, (n32 + 3u) & ~3u);
+
+    // transform.cpp:363-384: per symbol encode (path before update), then update
+    auto code = [&](uint32_t sym) {
+        uint32_t s = uni(fgk.T.where[sym]);
+        uint64_t rev = 0;
+        uint32_t d = 0;
+        const uint32_t fresh = s == 0;
+        if (fresh) s = uni(fgk.split(sym));  // path recorded from the old NYT (level 1)
+        fgk.template update<true>(s, fresh, rev, d);
+        // rev holds the leaf-level bit at bit 0 and the root's child at bit d-1: read MSB
+        // first it is the root-to-leaf code
+        if (d) sink.put64(rev, d);
+        if (fresh) sink.put(sym, 8);  // huffman.cpp:44-50: NYT code + 8 raw bits
+        ++nsym;
+    };
+
+    uint32_t prev = 0, run_byte = 0, run = 0;
+    uint32_t next = buf_load(rin, lane * 4);
+    for (uint32_t base = 0; base < n32 && !fgk.bad; base += 256) {
+        const uint32_t chunk = next;
+        next = buf_load(rin, base + 256 + lane * 4);  // out of range past the end: reads 0
+        const uint32_t m = min(256u, n32 - base);
+        uint32_t word = 0;
+        for (uint32_t j = 0; j < m && !fgk.bad; ++j) {
+            if ((j & 3u) == 0) word = lane_read(chunk, j >> 2);
+            const uint32_t x = (word >> (8 * (j & 3u))) & 255u;
+            if (kSrc == SRC_SYMBOLS) {
+                code(x);
+                continue;
+            }
+            // transform.cpp:220-229 (diff) then transform.cpp:241-279 (MNP-5 RLE)
+            const uint32_t c = kSrc == SRC_RAW_DIFF ? ((x - prev) & 255u) : x;
+            prev = x;
+            const bool last = base + j + 1 == n32;
+            uint32_t q, nq;  // up to two symbols, first in the low byte
+            if (run != 0 && c == run_byte && !last) {
+                ++run;
+                nq = (run <= 3 || run == 258) ? 1u : 0u;
+                q = run == 258 ? 255u : c;
+                run = run == 258 ? 0u : run;
+            } else {
+                nq = run >= 3 ? 2u : 1u;
+                q = run >= 3 ? ((run - 3) | (c << 8)) : c;
+                run_byte = c;
+                run = 1;
+            }
+            for (; nq; --nq, q >>= 8) code(q & 255u);
+        }
+    }
+
+    const uint64_t total = sink.finish();
+    const uint32_t st = fgk.bad ? (uint32_t)HC_ERR_DEVICE : (total <= cap ? 0u : (uint32_t)HC_ERR_CAPACITY);
+    // headers.cpp:110-116: u64 little-endian symbol count in words 0-1 (lanes 0 and 1 stored
+    // those words first, so this store is ordered after theirs)
+    buf_store(sink.rs, lane < 2 ? lane * 4 : kDrop, lane ? (uint32_t)(nsym >> 32) : (uint32_t)nsym);
+    if (lane == 0) {
+        bt.out_lens[sid] = fgk.bad ? 0 : total;
+        bt.status[sid] = (int32_t)st;
+    }
+}
+
+// --------------------------------------------------------------------------- the decoder --
+
+// MSB-first reader over a stream's bytes; words come from a 64-word VGPR chunk.
+struct BitSource {
+    rsrc_t rs;
+    uint32_t lane;
+    uint32_t cbase;  // byte offset of chunk lane 0
+    uint32_t chunk;
+    uint32_t ridx;
+    uint64_t win;    // upcoming bits, MSB-aligned
+    uint32_t nwin;
+    uint64_t loaded; // bits moved into win so far (from stream bit 0)
+
+    __device__ __forceinline__ void refill()
+    {
+        const uint32_t w = __builtin_bswap32(lane_read(chunk, ridx));
+        win |= (uint64_t)w << (32 - nwin);
+        nwin += 32;
+        loaded += 32;
+        if (++ridx == 64) {
+            cbase += 256;
+            chunk = buf_load(rs, cbase + lane * 4);
+            ridx = 0;
+        }
+    }
+    __device__ __forceinline__ uint32_t bit()
+    {
+        if (nwin == 0) refill();
+        const uint32_t b = (uint32_t)(win >> 63);
+        win <<= 1;
+        --nwin;
+        return b;
+    }
+    __device__ __forceinline__ uint32_t bits8()
+    {
+        if (nwin < 8) refill();
+        const uint32_t b = (uint32_t)(win >> 56);
+        win <<= 8;
+        nwin -= 8;
+        return b;
+    }
+};
+
+// VGPR byte stage for decoded output: 256 bytes per coalesced buffer store.
+struct ByteSink {
+    rsrc_t rs;
+    uint32_t lane;
+    uint64_t pos;  // bytes produced (may exceed the capacity: then only counted)
+    uint32_t cur;  // partial word
+    uint32_t stage;
+
+    __device__ __forceinline__ void byte(uint32_t b)
+    {
+        cur |= b << (8 * (uint32_t)(pos & 3));
+        ++pos;
+        if ((pos & 3) == 0) {
+            stage = lane == (((uint32_t)(pos >> 2) - 1) & 63u) ? cur : stage;
+            cur = 0;
+            if ((pos & 255) == 0) {
+                const uint64_t wi = (pos >> 2) - 64 + lane;
+                buf_store(rs, wi < (kMaxBufBytes >> 2) ? (uint32_t)wi * 4 : kDrop, stage);
+            }
+        }
+    }
+    __device__ __forceinline__ void finish()
+    {
+        const uint64_t wbase = (pos >> 2) & ~63ull;
+        const uint32_t full = (uint32_t)((pos >> 2) & 63);
+        const uint32_t tail = (uint32_t)(pos & 3);
+        const uint64_t wi = wbase + lane;
+        const bool ok = wi < (kMaxBufBytes >> 2);
+        buf_store(rs, ok && lane < full ? (uint32_t)wi * 4 : kDrop, stage);
+        for (uint32_t b = 0; b < 3; ++b)
+            buf_store8(rs, ok && lane == full && b < tail ? (uint32_t)wi * 4 + b : kDrop, cur >> (8 * b));
+    }
+};
+
+template <bool kWide, int kDst>
+__global__ __launch_bounds__(256) void decode_kernel(Batch bt)
+{
+    __shared__ Tree<kWide> trees[kWaves];
+    const uint32_t lane = lane_id();
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t sid = blockIdx.x * kWaves + wv;
+    if (sid >= bt.n) return;
+
+    const uint64_t in_off = uni64(bt.in_offs[sid]);
+    const uint64_t len = uni64(bt.in_lens[sid]);
+    const uint64_t cap = uni64(bt.out_caps[sid]);
+    const uint32_t len32 = (uint32_t)min(len, (uint64_t)kMaxBufBytes);
+    const rsrc_t rin = make_rsrc(bt.in + in_off, (len32 + 3u) & ~3u);
+    const uint32_t hdr = buf_load(rin, lane * 4);  // words 0..63 of the stream
+    uint32_t st = 0;
+    uint64_t count = 0;
+    uint32_t flags = 0;
+    if (len < 9) {
+        st = HC_ERR_HEADER;  // main.cpp:99-104
+    } else {
+        count = (uint64_t)lane_read(hdr, 0) | ((uint64_t)lane_read(hdr, 1) << 32);
+        flags = lane_read(hdr, 2) & 255u;
+        const uint64_t avail = (len - 9) * 8;
+        // the first symbol costs >= 8 bits and each later one >= 1: a larger count cannot
+        // decode, and the reference ends such a stream with status 9 (transform.cpp:394-398)
+        if (count > (avail >= 8 ? avail - 7 : 0)) st = HC_ERR_HUFFMAN;
+        else if (kDst == DST_RAW && (flags & 0x40u)) st = HC_ERR_UNSUPPORTED;
+        else if (count > kWideMaxSymbols || len > kMaxBufBytes) st = HC_ERR_UNSUPPORTED;
+    }
+    const bool narrow_ok = count <= kNarrowMaxSymbols;
+    if (st == 0 && kWide == narrow_ok) return;  // the other variant's launch owns it
+    if (st != 0) {
+        if (!kWide && lane == 0) {
+            bt.status[sid] = (int32_t)st;
+            bt.out_lens[sid] = 0;
+        }
+        return;
+    }
+
+    Fgk<kWide> fgk(trees[wv], lane);
+    BitSource in;
+    in.rs = rin;
+    in.lane = lane;
+    in.cbase = 0;
+    in.chunk = hdr;
+    in.ridx = 2;
+    in.win = 0;
+    in.nwin = 0;
+    in.loaded = 64;
+    in.refill();  // word 2: flags byte + first payload bits
+    in.win <<= 8;
+    in.nwin -= 8;
+    const uint64_t avail_end = len * 8;  // stream bit index one past the last payload bit
+
+    ByteSink out;
+    out.rs = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
+    out.lane = lane;
+    out.pos = 0;
+    out.cur = 0;
+    out.stage = 0;
+
+    const bool diff = kDst == DST_RAW && (flags & 0x80u);
+    uint32_t prev = 0, run_byte = 0, run = 0;
+    uint64_t no_rev = 0;
+    uint32_t no_d = 0;
+
+    for (uint64_t i = 0; i < count; ++i) {
+        // huffman.cpp:60-93: walk down from the root
+        uint32_t x = kRoot;
+        uint32_t b = uni(fgk.T.body[x]);
+        while (b & kInner) {
+            const uint32_t nx = (b & 255u) * 2 + in.bit();
+            if (nx >= x) {  // children sit below their parent: anything else is corruption
+                fgk.bad = 1;
+                break;
+            }
+            x = nx;
+            b = uni(fgk.T.body[x]);
+        }
+        if (fgk.bad) break;
+        uint32_t sym;
+        if (b & kNyt) {
+            sym = in.bits8();
+            x = uni(fgk.split(sym));
+        } else {
+            sym = b & 255u;
+        }
+        if (in.loaded - in.nwin > avail_end) {  // ran past the payload: transform.cpp:394-398
+            st = HC_ERR_HUFFMAN;
+            break;
+        }
+        fgk.template update<false>(x, 0, no_rev, no_d);
+        if (fgk.bad) break;
+
+        if (kDst == DST_SYMBOLS) {
+            out.byte(sym);
+            continue;
+        }
+        // transform.cpp:137-159 (RLE revert), then transform.cpp:231-239 (diff revert)
+        if (run == 3) {
+            for (uint32_t r = 0; r < sym; ++r) {
+                prev = diff ? ((prev + run_byte) & 255u) : run_byte;
+                out.byte(prev);
+            }
+            run = 0;
+        } else {
+            prev = diff ? ((prev + sym) & 255u) : sym;
+            out.byte(prev);
+            run = sym == run_byte ? run + 1 : 1;
+            run_byte = sym;
+        }
+    }
+    if (fgk.bad) st = HC_ERR_DEVICE;
+    if (st == 0) out.finish();
+    if (st == 0 && out.pos > cap) st = HC_ERR_CAPACITY;
+    if (lane == 0) {
+        bt.status[sid] = (int32_t)st;
+        bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? out.pos : 0;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_encode(const Batch &b, EncSrc src, hipStream_t st)
+{
+    if (b.n == 0) return hipSuccess;
+    const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
+    switch (src) {
+    case SRC_RAW:
+        encode_kernel<false, SRC_RAW><<<grid, block, 0, st>>>(b);
+        encode_kernel<true, SRC_RAW><<<grid, block, 0, st>>>(b);
+        break;
+    case SRC_RAW_DIFF:
+        encode_kernel<false, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
+        encode_kernel<true, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
+        break;
+    default:
+        encode_kernel<false, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
+        encode_kernel<true, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
+        break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_decode(const Batch &b, DecDst dst, hipStream_t st)
+{
+    if (b.n == 0) return hipSuccess;
+    const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
+    if (dst == DST_RAW) {
+        decode_kernel<false, DST_RAW><<<grid, block, 0, st>>>(b);
+        decode_kernel<true, DST_RAW><<<grid, block, 0, st>>>(b);
+    } else {
+        decode_kernel<false, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        decode_kernel<true, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace hc

@@ -1,0 +1,52 @@
+// hc_internal.h — launchers shared between the kernel translation units and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hcodec.h"
+
+namespace hc {
+
+// One batch of independent streams. All pointers are device pointers.
+struct Batch {
+    const uint8_t *in;
+    const uint64_t *in_offs;
+    const uint64_t *in_lens;
+    uint32_t n;
+    uint8_t *out;
+    const uint64_t *out_offs;
+    const uint64_t *out_caps;
+    uint64_t *out_lens;
+    int32_t *status;
+    uint32_t flags;  // header flags byte for SRC_SYMBOLS encodes
+};
+
+enum EncSrc { SRC_RAW = 0, SRC_RAW_DIFF = 1, SRC_SYMBOLS = 2 };
+enum DecDst { DST_RAW = 0, DST_SYMBOLS = 1 };
+
+// Largest FGK symbol count the packed ("narrow") tree layout handles: weights live in 22 bits.
+constexpr uint64_t kNarrowMaxSymbols = (1ull << 22) - 2;
+// Largest count of the wide layout (32-bit weights, sentinel 0xFFFFFFFF).
+constexpr uint64_t kWideMaxSymbols = 0xFFFFFFFFull - 1;
+
+// fused [diff] -> RLE -> FGK encode, or FGK over a ready symbol stream (adaptive path)
+hipError_t launch_encode(const Batch &b, EncSrc src, hipStream_t st);
+// fused FGK decode -> RLE revert -> [diff revert] (diff taken from each stream's flags byte),
+// or FGK decode to the symbol stream
+hipError_t launch_decode(const Batch &b, DecDst dst, hipStream_t st);
+
+// adaptive block RLE (hc_adapt.hip); single matrix per call
+struct AdaptPlan;
+hipError_t adapt_encode(const uint8_t *d_matrix, uint64_t width, uint64_t height, uint8_t *d_out,
+                        uint64_t *d_out_len, uint64_t *h_block, hipStream_t st);
+hipError_t adapt_bound(uint64_t n, uint64_t width, uint64_t *bytes);
+// symbols -> matrix. Returns status via *h_status (host, synchronous).
+hipError_t adapt_decode(const uint8_t *d_sym, uint64_t nsym, uint8_t **d_matrix, uint64_t *h_len,
+                        int *h_status, hipStream_t st);
+
+// elementwise helpers (hc_adapt.hip)
+hipError_t diff_apply(uint8_t *d, uint64_t n, hipStream_t st);
+hipError_t diff_revert(uint8_t *d, uint64_t n, hipStream_t st);
+
+}  // namespace hc

@@ -1,0 +1,187 @@
+"""ctypes binding to libhcodec.so (include/hcodec.h, include/hcodec_synth.h).
+
+Host-side mirror of the reference's buffer-level interface (huffCompress / huffDecompress,
+src/main.cpp:39-128) plus the batched device entry points. Torch is used only for device memory
+and streams (tensors are passed by data_ptr()). There is deliberately no CPU fallback: if the
+shared library is missing, every call raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libhcodec.so")
+CLI_PATH = os.path.join(PKG, "bin", "huffman-codec")
+INCLUDE_DIR = os.path.join(os.path.dirname(PKG), "include")
+
+HC_OK = 0
+HC_ERR_WIDTH = 4
+HC_ERR_MATRIX_SIZE = 6
+HC_ERR_HEADER = 8
+HC_ERR_HUFFMAN = 9
+HC_ERR_ADAPT_HEADER = 10
+HC_ERR_ADAPT_DIRS = 11
+HC_ERR_DIMS = 12
+HC_ERR_BLOCK_DATA = 13
+HC_ERR_BLOCK_EOF = 14
+HC_ERR_LEFTOVER = 15
+HC_ERR_CAPACITY = 64
+HC_ERR_UNSUPPORTED = 65
+HC_ERR_BLOCK_SIZE = 66
+HC_ERR_TOO_LARGE = 67
+HC_ERR_DEVICE = 70
+HC_ERR_ARG = 71
+
+HC_FLAG_DIFF = 0x80
+HC_FLAG_ADAPT = 0x40
+
+SYNTH = {"noise": 0, "grad": 1, "photo": 2}
+
+_lib = None
+
+
+class HCodecError(RuntimeError):
+    pass
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", PKG], check=True)
+
+
+def lib():
+    """Load libhcodec.so; raise if it has not been built (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HCodecError(f"{LIB_PATH} missing: build it with `make -C {PKG}`")
+    # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's). Whichever loads first
+    # serves the whole process; loading ours first leaves torch without a GPU. So let torch's
+    # runtime load first and libhcodec.so binds to it: one HIP runtime, shared device pointers.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.c_void_p
+    u64 = ctypes.c_uint64
+    vp = ctypes.c_void_p
+    L.hc_compress_bound.argtypes = [u64, ctypes.c_int]
+    L.hc_compress_bound.restype = u64
+    L.hc_compress.argtypes = [u8p, u64, ctypes.c_int, ctypes.c_int, u64, u8p, u64,
+                              ctypes.POINTER(u64)]
+    L.hc_decompress.argtypes = [u8p, u64, u8p, u64, ctypes.POINTER(u64)]
+    L.hc_decompress_alloc.argtypes = [u8p, u64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u64)]
+    L.hc_free.argtypes = [vp]
+    L.hc_compress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
+                                    vp, vp]
+    L.hc_decompress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
+    L.hc_version.restype = ctypes.c_char_p
+    L.hc_device_ok.restype = ctypes.c_int
+    L.hc_device_info.argtypes = [ctypes.c_char_p, u64]
+    L.hc_device_info.restype = ctypes.c_int
+    L.hc_synth_batch.argtypes = [ctypes.c_int, u64, ctypes.c_uint32, u64, u64, vp, u64, vp]
+    _lib = L
+    return L
+
+
+def _buf(data):
+    b = bytes(data)
+    return b, ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) if b else None
+
+
+def compress(data, use_diff=False, use_adapt=False, width=512):
+    """hc_compress: (status, encoded bytes). Mirrors huffCompress (main.cpp:39-87)."""
+    b, p = _buf(data)
+    cap = lib().hc_compress_bound(len(b), int(bool(use_adapt)))
+    out = ctypes.create_string_buffer(max(int(cap), 1))
+    n = ctypes.c_uint64(0)
+    st = lib().hc_compress(p, len(b), int(bool(use_diff)), int(bool(use_adapt)), width,
+                           ctypes.cast(out, ctypes.c_void_p), cap, ctypes.byref(n))
+    return st, (out.raw[:n.value] if st == 0 else b"")
+
+
+def decompress(data):
+    """hc_decompress_alloc: (status, decoded bytes). Mirrors huffDecompress (main.cpp:90-128)."""
+    b, p = _buf(data)
+    q = ctypes.c_void_p()
+    n = ctypes.c_uint64(0)
+    st = lib().hc_decompress_alloc(p, len(b), ctypes.byref(q), ctypes.byref(n))
+    out = b""
+    if st == 0:
+        out = ctypes.string_at(q, n.value) if n.value else b""
+    if q:
+        lib().hc_free(q)
+    return st, out
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _dp(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def compress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status,
+                   use_diff=False, stream=None):
+    """hc_compress_batch on torch CUDA tensors (uint8 data, int64 offsets/lengths, int32 status)."""
+    n = in_offs.numel()
+    rc = lib().hc_compress_batch(_dp(inp), _dp(in_offs), _dp(in_lens), n,
+                                 HC_FLAG_DIFF if use_diff else 0, _dp(out), _dp(out_offs),
+                                 _dp(out_caps), _dp(out_lens), _dp(status), _stream_handle(stream))
+    if rc:
+        raise HCodecError(f"hc_compress_batch failed: {rc}")
+
+
+def decompress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status, stream=None):
+    n = in_offs.numel()
+    rc = lib().hc_decompress_batch(_dp(inp), _dp(in_offs), _dp(in_lens), n, _dp(out),
+                                   _dp(out_offs), _dp(out_caps), _dp(out_lens), _dp(status),
+                                   _stream_handle(stream))
+    if rc:
+        raise HCodecError(f"hc_decompress_batch failed: {rc}")
+
+
+def synth_batch(kind, k0, n_streams, width, height, out, stride, stream=None):
+    """hc_synth_batch: SURVEY.md Appendix D inputs generated in device memory."""
+    rc = lib().hc_synth_batch(SYNTH.get(kind, kind), k0, n_streams, width, height, _dp(out),
+                              stride, _stream_handle(stream))
+    if rc:
+        raise HCodecError(f"hc_synth_batch failed: {rc}")
+
+
+def compress_bound(n, use_adapt=False):
+    return int(lib().hc_compress_bound(n, int(bool(use_adapt))))
+
+
+def device_ok():
+    return bool(lib().hc_device_ok())
+
+
+def device_info():
+    buf = ctypes.create_string_buffer(512)
+    lib().hc_device_info(buf, 512)
+    return buf.value.decode()
+
+
+def version():
+    return lib().hc_version().decode()
+
+
+def header_symbols():
+    """Every function name declared in include/*.h (the exported surface)."""
+    import re
+    names = []
+    for fn in sorted(os.listdir(INCLUDE_DIR)):
+        if fn.endswith(".h"):
+            txt = open(os.path.join(INCLUDE_DIR, fn)).read()
+            txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+            names += re.findall(r"\b(hc_[a-z0-9_]+)\s*\(", txt)
+    return sorted(set(names))

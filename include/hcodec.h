@@ -1,0 +1,110 @@
+/*
+ * hcodec.h — C ABI of the MI355X-native huffman-codec pipeline (libhcodec.so).
+ *
+ * Drop-in boundary for dominiksalvet/huffman-codec's codec path. The reference is one C++
+ * binary with no library; its replaceable seams are the buffer functions huffCompress /
+ * huffDecompress (src/main.cpp:39-87, src/main.cpp:90-128), which main() calls at
+ * src/main.cpp:211-215, and the CLI contract around them (src/main.cpp:152-221, reproduced by
+ * the `huffman-codec` binary built from huffman-codec_amd/csrc/hc_cli.cpp).
+ *
+ * Everything here is plain C: pointers and sizes, no torch or HIP types in the signatures
+ * (a hipStream_t is passed as void*). Every entry point is re-entrant: no hidden global state.
+ * Compute runs on the current HIP device; there is no CPU fallback — without a usable gfx950
+ * device every compute entry point returns HC_ERR_DEVICE.
+ *
+ * Status codes are the reference's process exit codes: the reference calls
+ * exit(n) deep inside its library; here n is returned instead, per call or per stream.
+ */
+#ifndef HCODEC_H
+#define HCODEC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum hc_status {
+    HC_OK = 0,
+    HC_ERR_WIDTH = 4,         /* main.cpp:195-199  width 0 when compressing                  */
+    HC_ERR_MATRIX_SIZE = 6,   /* main.cpp:54-58    input size not a multiple of width (-a)   */
+    HC_ERR_HEADER = 8,        /* main.cpp:99-104   missing <64b-count><8b-flags> header      */
+    HC_ERR_HUFFMAN = 9,       /* transform.cpp:394-398  FGK bits exhausted                   */
+    HC_ERR_ADAPT_HEADER = 10, /* headers.cpp:67-71  adaptive header shorter than 24 bytes   */
+    HC_ERR_ADAPT_DIRS = 11,   /* headers.cpp:94-98  missing scan-direction bytes             */
+    HC_ERR_DIMS = 12,         /* transform.cpp:300-304  width or height < 8 (-a)             */
+    HC_ERR_BLOCK_DATA = 13,   /* transform.cpp:178-182  block RLE overshoots its block       */
+    HC_ERR_BLOCK_EOF = 14,    /* transform.cpp:170-174  block RLE data ends early            */
+    HC_ERR_LEFTOVER = 15,     /* transform.cpp:354-358  bytes left after the last block      */
+    /* beyond the reference (it has no equivalent, or crashes) */
+    HC_ERR_CAPACITY = 64,     /* output capacity too small; the needed length is reported    */
+    HC_ERR_UNSUPPORTED = 65,  /* stream beyond the device coder's limits (>= 2^32-1 symbols) */
+    HC_ERR_BLOCK_SIZE = 66,   /* forged adaptive header, block size 0 (reference: SIGFPE)    */
+    HC_ERR_TOO_LARGE = 67,    /* forged adaptive header, W*H > 2^36 (reference: bad_alloc)   */
+    HC_ERR_DEVICE = 70,       /* HIP runtime error / no gfx950 device                        */
+    HC_ERR_ARG = 71           /* null pointer, misaligned device buffer, bad flag            */
+};
+
+/* Flags byte of the outer header (headers.cpp:118-122): bit 7 diff model, bit 6 adaptive RLE */
+#define HC_FLAG_DIFF 0x80u
+#define HC_FLAG_ADAPT 0x40u
+
+/* ---------------------------------------------------------------------------------------
+ * Single-buffer API — host buffers, synchronous. Replaces huffCompress (main.cpp:39-87) and
+ * huffDecompress (main.cpp:90-128); the input is a byte buffer instead of an ifstream.
+ * ------------------------------------------------------------------------------------- */
+
+/* Worst-case compressed size of an in_len-byte input (any mode). */
+uint64_t hc_compress_bound(uint64_t in_len, int use_adapt);
+
+/* huffCompress(ifs, useDiffModel, useAdaptRLE, matrixWidth). Writes the whole stream
+ * (<u64 LE count><u8 flags><FGK bits>) to out. Returns HC_OK, HC_ERR_WIDTH (width == 0, the
+ * CLI check of main.cpp:195-199), HC_ERR_MATRIX_SIZE, HC_ERR_DIMS, HC_ERR_CAPACITY (out_cap <
+ * result; *out_len = needed), HC_ERR_UNSUPPORTED, HC_ERR_DEVICE or HC_ERR_ARG. */
+int hc_compress(const uint8_t *in, uint64_t in_len, int use_diff, int use_adapt, uint64_t width,
+                uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* huffDecompress(ifs). Returns HC_OK, 8, 9, 10, 11, 13, 14, 15, HC_ERR_CAPACITY (out_cap too
+ * small; *out_len = needed), HC_ERR_BLOCK_SIZE, HC_ERR_TOO_LARGE, HC_ERR_DEVICE or HC_ERR_ARG. */
+int hc_decompress(const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t out_cap,
+                  uint64_t *out_len);
+
+/* Same, with the output allocated by the library (release with hc_free). */
+int hc_decompress_alloc(const uint8_t *in, uint64_t in_len, uint8_t **out, uint64_t *out_len);
+void hc_free(void *p);
+
+/* ---------------------------------------------------------------------------------------
+ * Batched device API — many independent streams per call, asynchronous on `stream`
+ * (a hipStream_t; NULL = default stream). All pointers are DEVICE pointers. Stream i reads
+ * in[in_offs[i] .. +in_lens[i]) and writes out[out_offs[i] .. +out_caps[i]); every
+ * in + in_offs[i] and out + out_offs[i] must be 4-byte aligned. Per-stream results land in
+ * out_lens[i] (bytes written, or bytes needed on HC_ERR_CAPACITY) and status[i].
+ * The return value reports argument / launch errors only.
+ * ------------------------------------------------------------------------------------- */
+
+/* Compress n_streams raw streams: [diff model] -> MNP-5 RLE -> FGK -> header, fused in one
+ * kernel (one stream per wavefront). flags: 0 or HC_FLAG_DIFF (adaptive streams go through
+ * hc_compress). Capacity per stream: hc_compress_bound(in_len, 0) always suffices. */
+int hc_compress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                      uint32_t n_streams, uint32_t flags, uint8_t *out, const uint64_t *out_offs,
+                      const uint64_t *out_caps, uint64_t *out_lens, int32_t *status,
+                      void *stream);
+
+/* Decompress n_streams encoded streams (non-adaptive: a stream whose flags byte has bit 6 set
+ * gets HC_ERR_UNSUPPORTED here; use hc_decompress). FGK -> RLE revert -> [diff revert], fused. */
+int hc_decompress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                        uint32_t n_streams, uint8_t *out, const uint64_t *out_offs,
+                        const uint64_t *out_caps, uint64_t *out_lens, int32_t *status,
+                        void *stream);
+
+/* Library version string and a device check (1 = a gfx950 device is usable). */
+const char *hc_version(void);
+int hc_device_ok(void);
+/* Human-readable device / runtime description (or the HIP error that prevents one) into buf;
+ * returns hc_device_ok(). */
+int hc_device_info(char *buf, uint64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HCODEC_H */
