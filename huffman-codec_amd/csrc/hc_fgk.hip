@@ -29,7 +29,7 @@ namespace hc {
 namespace {
 
 constexpr uint32_t kRoot = 512;
-constexpr uint32_t kWords = 516;  // positions 0..512 + sentinels 513..515
+constexpr uint32_t kWords = 576;  // positions 0..512 + sentinels 513..575 (s + 63)
 constexpr uint32_t kInner = 0x100;
 constexpr uint32_t kNyt = 0x200;
 constexpr int kWaves = 4;
@@ -40,9 +40,9 @@ template <bool kWide>
 struct alignas(16) Tree {
     uint32_t wt[kWords];              // narrow: weight << 10 | parent; wide: weight
     uint32_t scratch[64];             // landing words of lanes that must not write
-    uint16_t body[kWords];            // symbol | kInner + child pair | kNyt
+    uint16_t body[516];               // symbol | kInner + child pair | kNyt
     uint16_t where[256];              // symbol -> position, 0 = not yet transmitted
-    uint16_t up[kWide ? kWords : 8];  // wide: parent position
+    uint16_t up[kWide ? 516 : 8];     // wide: parent position
 };
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -95,8 +95,8 @@ struct Fgk {
     __device__ Fgk(Tree<kWide> &t, uint32_t l) : T(t), lane(l), nyt(kRoot), rootw(0), bad(0)
     {
         // huffman.cpp:23-31: a lone NYT root
-        for (uint32_t i = lane; i < kWords; i += 64) {
-            T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
+        for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
+        for (uint32_t i = lane; i < 516; i += 64) {
             T.body[i] = i == kRoot ? kNyt : 0;
             if (kWide) T.up[i] = 0;
         }
@@ -153,73 +153,98 @@ struct Fgk {
     }
 
     // highest position >= from whose weight equals that of word w, when positions
-    // from-64..from-1 all had it
+    // from-64..from-1 all had it (the sentinels above the root end the scan)
     __device__ uint32_t leader_far(uint32_t from, uint32_t w)
     {
         const uint32_t lim = kWide ? w : (w | 1023u);
         for (;;) {
-            const uint32_t a = min(from + lane, kWords - 1);
-            const uint64_t le = ballot(T.wt[a] <= lim);
+            const uint64_t le = ballot(T.wt[min(from + lane, kWords - 1)] <= lim);
             if (le != ~0ull) return from + (uint32_t)__builtin_ctzll(~le) - 1;
             from += 64;
         }
     }
 
-    // huffman.cpp:95-128 (update) from position s upward. With kRecord, also collects the
-    // PRE-update code of the path (huffman.cpp:136-155) into rev (bit i = level i above the
-    // leaf) for levels >= first; on the first swap the rest of the old path is read before
-    // the tree changes above it.
-    template <bool kRecord>
-    __device__ __forceinline__ void update(uint32_t s, uint32_t first, uint64_t &rev, uint32_t &d)
+    __device__ __forceinline__ uint32_t parent(uint32_t x) const
     {
-        bool rec = kRecord;
-        uint32_t lvl = 0;
-        while (s != kRoot) {
-            const uint32_t a = min(s + lane, kWords - 1);
-            const uint32_t v = T.wt[a];
+        return kWide ? uni(T.up[x]) : (uni(T.wt[x]) & 1023u);
+    }
+
+    // Encoder: the path from position s to the root, BEFORE the update (the code of
+    // huffman.cpp:136-155): the position of level k (0 = s) goes to lane k; returns the levels.
+    __device__ __forceinline__ uint32_t chase(uint32_t s, uint32_t &pv)
+    {
+        uint32_t k = 0;
+        pv = kRoot + 1;
+        do {
+            pv = lane == k ? s : pv;
+            ++k;
+            s = max(parent(s), s + 1);  // parents sit above children; max() bounds a bug
+        } while (s < kRoot);
+        bad |= (s ^ kRoot) | (k > 64 ? 1u : 0u);
+        return k;
+    }
+
+    // huffman.cpp:95-128 (update), serial form, from position s upward: per level one
+    // lane-parallel read of positions s..s+63, one ballot (the trailing-ones count of
+    // "weight == w[s]" is the block leader, highest number first), a swap when the leader is
+    // neither s nor its parent, one store.
+    __device__ void walk(uint32_t s)
+    {
+        for (;;) {
+            const uint32_t v = T.wt[s + lane];  // sentinels cover s + 63 <= 575
             uint32_t ws = uni(v);
-            // positions >= s weigh >= w[s]; "same weight" = "word <= w[s] with all low bits"
             const uint64_t le = ballot(v <= (kWide ? ws : (ws | 1023u)));
             uint32_t p = kWide ? uni(T.up[s]) : (ws & 1023u);
-            if (kRecord && rec && lvl >= first) {
-                rev |= (uint64_t)(s & 1u) << d;
-                ++d;
-            }
-            const uint32_t lead = le != ~0ull ? s + (uint32_t)__builtin_ctzll(~le) - 1 : leader_far(s + 64, ws);
-            if (lead != s && lead != p) {
-                if (kRecord && rec) {  // finish the old code path first (read-only walk)
-                    for (uint32_t x = p; x != kRoot;) {
-                        rev |= (uint64_t)(x & 1u) << d;
-                        ++d;
-                        const uint32_t nx = kWide ? uni(T.up[x]) : (uni(T.wt[x]) & 1023u);
-                        if (nx <= x || d >= 64) {
-                            bad = 1;
-                            return;
-                        }
-                        x = nx;
-                    }
-                    rec = false;
+            if ((uint32_t)le & 2u) {  // s+1 weighs the same: find the block leader
+                const uint32_t lead =
+                    ~le ? s + (uint32_t)__builtin_ctzll(~le) - 1 : leader_far(s + 64, ws);
+                if (lead != p) {
+                    swap(s, lead);
+                    // the swap rewrites only parent fields below s and lead, never their own
+                    // words, so the pre-swap read still holds lead's word when in range
+                    const uint32_t off = lead - s;
+                    ws = off < 64 ? lane_read(v, off) : uni(T.wt[lead]);
+                    s = lead;
+                    p = kWide ? uni(T.up[s]) : (ws & 1023u);
                 }
-                swap(s, lead);
-                // the swap rewrites only the parent fields below s and lead, never their own
-                // words, so the pre-swap read still holds lead's word when it was in range
-                const uint32_t off = lead - s;
-                ws = off < 64 ? lane_read(v, off) : uni(T.wt[lead]);
-                s = lead;
-                p = kWide ? uni(T.up[s]) : (ws & 1023u);
             }
             *(lane == 0 ? &T.wt[s] : scr32()) = ws + kInc;
             __builtin_amdgcn_wave_barrier();
-            if (p <= s) {  // parents sit above their children: anything else is corruption
-                bad = 1;
-                return;
-            }
-            s = p;
-            ++lvl;
+            s = max(p, s + 1);
+            if (s >= kRoot) break;
         }
+        bad |= s ^ kRoot;
         rootw += kInc;
         *(lane == 0 ? &T.wt[kRoot] : scr32()) = rootw;
         __builtin_amdgcn_wave_barrier();
+    }
+
+    // The same update when the path is already known: lanes lo..hi hold the positions of
+    // levels 0..hi-lo. Until the first swap the tree does not change, so every level's leader
+    // test reads the pre-update weights in parallel: a node leads its block when the next
+    // position is heavier, or when that position is its parent and the one after is heavier.
+    // Levels below the first one that fails increment with one store; the serial walk takes
+    // over from there (it also bumps the root).
+    __device__ __forceinline__ void update_path(uint32_t pv, uint32_t lo, uint32_t hi)
+    {
+        const bool act = lane >= lo && lane <= hi;
+        const uint32_t a = act ? pv : kRoot + 1;
+        const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1], w2 = T.wt[a + 2];
+        const uint32_t par = kWide ? T.up[a] : (w0 & 1023u);
+        const uint32_t lim = kWide ? w0 : (w0 | 1023u);
+        // no short-circuit: every term is computed, nothing branches per lane
+        const uint32_t ok = (uint32_t)(w1 > lim) | ((uint32_t)(a + 1 == par) & (uint32_t)(w2 > lim));
+        const uint64_t fail = ballot(act & !ok);
+        const uint32_t k = fail ? (uint32_t)__builtin_ctzll(fail) : hi + 1;
+        *(lane >= lo && lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
+        __builtin_amdgcn_wave_barrier();
+        if (k <= hi) {
+            walk(lane_read(pv, k));
+        } else {
+            rootw += kInc;
+            *(lane == 0 ? &T.wt[kRoot] : scr32()) = rootw;
+            __builtin_amdgcn_wave_barrier();
+        }
     }
 };
 
@@ -327,24 +352,31 @@ __global__ __launch_bounds__(256) void encode_kernel(Batch bt)
     // transform.cpp:363-384: per symbol encode (path before update), then update
     auto code = [&](uint32_t sym) {
         uint32_t s = uni(fgk.T.where[sym]);
-        uint64_t rev = 0;
-        uint32_t d = 0;
         const uint32_t fresh = s == 0;
-        if (fresh) s = uni(fgk.split(sym));  // path recorded from the old NYT (level 1)
-        fgk.template update<true>(s, fresh, rev, d);
-        // rev holds the leaf-level bit at bit 0 and the root's child at bit d-1: read MSB
-        // first it is the root-to-leaf code
-        if (d) sink.put64(rev, d);
-        if (fresh) sink.put(sym, 8);  // huffman.cpp:44-50: NYT code + 8 raw bits
+        if (fresh) s = uni(fgk.split(sym));
+        uint32_t pv;
+        const uint32_t d = fgk.chase(s, pv);
+        // bit k = code bit (position parity, left = even) of level k; read MSB first it is the
+        // root-to-leaf code. A fresh symbol starts at its new leaf, one level below the NYT
+        // whose code is sent (huffman.cpp:44-50), so that lowest bit is dropped.
+        const uint64_t bits = ballot((pv & 1u) && lane < d);
+        fgk.update_path(pv, 0, d - 1);
+        if (d > fresh) sink.put64(bits >> fresh, d - fresh);
+        if (fresh) sink.put(sym, 8);  // NYT code + 8 raw bits
         ++nsym;
     };
 
-    uint32_t prev = 0, run_byte = 0, run = 0;
+    // transform.cpp:220-229 (diff) then transform.cpp:241-279 (MNP-5 RLE). run_byte = 0x100
+    // ("no run": at the start and after a 258-byte cut) folds the reference's run != 0 test
+    // into the byte compare; set right before the stream's final byte, it also sends that byte
+    // down the literal path as transform.cpp:252 does.
+    uint32_t prev = 0, run_byte = 0x100, run = 0;
     uint32_t next = buf_load(rin, lane * 4);
     for (uint32_t base = 0; base < n32 && !fgk.bad; base += 256) {
         const uint32_t chunk = next;
         next = buf_load(rin, base + 256 + lane * 4);  // out of range past the end: reads 0
         const uint32_t m = min(256u, n32 - base);
+        const uint32_t fin = base + m == n32 ? m - 1 : ~0u;  // index of the final byte, if here
         uint32_t word = 0;
         for (uint32_t j = 0; j < m && !fgk.bad; ++j) {
             if ((j & 3u) == 0) word = lane_read(chunk, j >> 2);
@@ -353,19 +385,21 @@ __global__ __launch_bounds__(256) void encode_kernel(Batch bt)
                 code(x);
                 continue;
             }
-            // transform.cpp:220-229 (diff) then transform.cpp:241-279 (MNP-5 RLE)
             const uint32_t c = kSrc == SRC_RAW_DIFF ? ((x - prev) & 255u) : x;
             prev = x;
-            const bool last = base + j + 1 == n32;
+            if (j == fin) run_byte = 0x100;
             uint32_t q, nq;  // up to two symbols, first in the low byte
-            if (run != 0 && c == run_byte && !last) {
+            if (c == run_byte) {
                 ++run;
-                nq = (run <= 3 || run == 258) ? 1u : 0u;
-                q = run == 258 ? 255u : c;
-                run = run == 258 ? 0u : run;
+                const uint32_t cut = run == 258 ? 1u : 0u;  // 255 + 3
+                nq = (run <= 3 ? 1u : 0u) | cut;
+                q = cut ? 255u : c;
+                run = cut ? 0u : run;
+                run_byte = cut ? 0x100u : run_byte;
             } else {
-                nq = run >= 3 ? 2u : 1u;
-                q = run >= 3 ? ((run - 3) | (c << 8)) : c;
+                const uint32_t cnt = run >= 3 ? 1u : 0u;
+                nq = 1 + cnt;
+                q = cnt ? ((run - 3) | (c << 8)) : c;
                 run_byte = c;
                 run = 1;
             }
@@ -393,16 +427,15 @@ struct BitSource {
     uint32_t cbase;  // byte offset of chunk lane 0
     uint32_t chunk;
     uint32_t ridx;
-    uint64_t win;    // upcoming bits, MSB-aligned
-    uint32_t nwin;
-    uint64_t loaded; // bits moved into win so far (from stream bit 0)
+    uint64_t win;  // upcoming bits, MSB-aligned
+    uint32_t nwin; // valid bits in win
 
+    // push the next 32 bits (needs nwin <= 32)
     __device__ __forceinline__ void refill()
     {
         const uint32_t w = __builtin_bswap32(lane_read(chunk, ridx));
         win |= (uint64_t)w << (32 - nwin);
         nwin += 32;
-        loaded += 32;
         if (++ridx == 64) {
             cbase += 256;
             chunk = buf_load(rs, cbase + lane * 4);
@@ -427,37 +460,34 @@ struct BitSource {
     }
 };
 
-// VGPR byte stage for decoded output: 256 bytes per coalesced buffer store.
+// VGPR byte stage for decoded output: 256 bytes per coalesced buffer store. pos may run past
+// the capacity (then bytes are only counted, the range check drops the stores).
 struct ByteSink {
     rsrc_t rs;
     uint32_t lane;
-    uint64_t pos;  // bytes produced (may exceed the capacity: then only counted)
+    uint32_t pos;  // bytes produced
     uint32_t cur;  // partial word
     uint32_t stage;
 
     __device__ __forceinline__ void byte(uint32_t b)
     {
-        cur |= b << (8 * (uint32_t)(pos & 3));
+        cur |= b << (8 * (pos & 3u));
         ++pos;
-        if ((pos & 3) == 0) {
-            stage = lane == (((uint32_t)(pos >> 2) - 1) & 63u) ? cur : stage;
+        if ((pos & 3u) == 0) {
+            stage = lane == ((pos >> 2) - 1) % 64u ? cur : stage;
             cur = 0;
-            if ((pos & 255) == 0) {
-                const uint64_t wi = (pos >> 2) - 64 + lane;
-                buf_store(rs, wi < (kMaxBufBytes >> 2) ? (uint32_t)wi * 4 : kDrop, stage);
-            }
+            if ((pos & 255u) == 0) buf_store(rs, pos - 256 + lane * 4, stage);
         }
     }
     __device__ __forceinline__ void finish()
     {
-        const uint64_t wbase = (pos >> 2) & ~63ull;
-        const uint32_t full = (uint32_t)((pos >> 2) & 63);
-        const uint32_t tail = (uint32_t)(pos & 3);
-        const uint64_t wi = wbase + lane;
-        const bool ok = wi < (kMaxBufBytes >> 2);
-        buf_store(rs, ok && lane < full ? (uint32_t)wi * 4 : kDrop, stage);
+        const uint32_t wbase = (pos >> 2) & ~63u;
+        const uint32_t full = (pos >> 2) & 63u;
+        const uint32_t tail = pos & 3u;
+        const uint32_t off = (wbase + lane) * 4;
+        buf_store(rs, lane < full ? off : kDrop, stage);
         for (uint32_t b = 0; b < 3; ++b)
-            buf_store8(rs, ok && lane == full && b < tail ? (uint32_t)wi * 4 + b : kDrop, cur >> (8 * b));
+            buf_store8(rs, lane == full && b < tail ? off + b : kDrop, cur >> (8 * b));
     }
 };
 
@@ -510,11 +540,10 @@ __global__ __launch_bounds__(256) void decode_kernel(Batch bt)
     in.ridx = 2;
     in.win = 0;
     in.nwin = 0;
-    in.loaded = 64;
     in.refill();  // word 2: flags byte + first payload bits
     in.win <<= 8;
     in.nwin -= 8;
-    const uint64_t avail_end = len * 8;  // stream bit index one past the last payload bit
+    uint64_t left = (len - 9) * 8;  // payload bits not consumed yet
 
     ByteSink out;
     out.rs = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
@@ -523,37 +552,56 @@ __global__ __launch_bounds__(256) void decode_kernel(Batch bt)
     out.cur = 0;
     out.stage = 0;
 
-    const bool diff = kDst == DST_RAW && (flags & 0x80u);
+    const uint32_t diff = kDst == DST_RAW && (flags & 0x80u);
     uint32_t prev = 0, run_byte = 0, run = 0;
-    uint64_t no_rev = 0;
-    uint32_t no_d = 0;
+    const uint32_t n = (uint32_t)count;
 
-    for (uint64_t i = 0; i < count; ++i) {
-        // huffman.cpp:60-93: walk down from the root
-        uint32_t x = kRoot;
-        uint32_t b = uni(fgk.T.body[x]);
+    for (uint32_t i = 0; i < n; ++i) {
+        // huffman.cpp:60-93: walk down from the root over a window of >= 33 bits; the visited
+        // positions go to lanes 63, 62, ... so that lanes lo..63 hold the path bottom-up
+        if (in.nwin <= 32) in.refill();
+        uint32_t x = kRoot, depth = 0, pv = kRoot + 1;
+        uint64_t w = in.win;
+        uint32_t b = uni(fgk.T.body[kRoot]);
         while (b & kInner) {
-            const uint32_t nx = (b & 255u) * 2 + in.bit();
-            if (nx >= x) {  // children sit below their parent: anything else is corruption
-                fgk.bad = 1;
-                break;
-            }
-            x = nx;
+            x = min((b & 255u) * 2 + (uint32_t)(w >> 63), x - 1);  // children sit below
+            w <<= 1;
+            pv = lane == 63 - depth ? x : pv;
+            ++depth;
             b = uni(fgk.T.body[x]);
         }
-        if (fgk.bad) break;
-        uint32_t sym;
+        if (depth <= in.nwin) {
+            in.win = w;
+            in.nwin -= depth;
+        } else {  // a code longer than the window (deep trees only): again, bit by bit
+            x = kRoot;
+            depth = 0;
+            pv = kRoot + 1;
+            b = uni(fgk.T.body[kRoot]);
+            while (b & kInner) {
+                x = min((b & 255u) * 2 + in.bit(), x - 1);
+                pv = lane == 63 - depth ? x : pv;
+                ++depth;
+                b = uni(fgk.T.body[x]);
+            }
+        }
+        uint32_t sym, used = depth;
         if (b & kNyt) {
             sym = in.bits8();
+            used += 8;
             x = uni(fgk.split(sym));
+            pv = lane == 63 - depth ? x : pv;
+            ++depth;
         } else {
             sym = b & 255u;
         }
-        if (in.loaded - in.nwin > avail_end) {  // ran past the payload: transform.cpp:394-398
+        if (used > left) {  // ran past the payload: transform.cpp:394-398
             st = HC_ERR_HUFFMAN;
             break;
         }
-        fgk.template update<false>(x, 0, no_rev, no_d);
+        left -= used;
+        if (depth > 63) fgk.bad = 1;
+        fgk.update_path(pv, 64 - depth, 63);
         if (fgk.bad) break;
 
         if (kDst == DST_SYMBOLS) {
@@ -572,6 +620,10 @@ __global__ __launch_bounds__(256) void decode_kernel(Batch bt)
             out.byte(prev);
             run = sym == run_byte ? run + 1 : 1;
             run_byte = sym;
+        }
+        if (out.pos > kMaxBufBytes) {  // beyond the 32-bit buffer offsets of the device path
+            st = HC_ERR_UNSUPPORTED;
+            break;
         }
     }
     if (fgk.bad) st = HC_ERR_DEVICE;
