@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=0, help="streams for the CPU baseline (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
+    ap.add_argument("--gather", action="store_true",
+                    help="after timing, gather every rank's encoded payloads into rank 0")
     return ap.parse_args()
 
 
@@ -53,7 +55,7 @@ def cpu_baseline(args, cores):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
-    sample = args.cpu_sample or 4 * cores
+    sample = args.cpu_sample or 8 * cores
     kind = "reference" if oracle.ref_available() else "port"
     raws = [oracle.synth(args.kind, k).tobytes() for k in range(sample)]
     mode = ["-c"] if args.no_diff else ["-c", "-m"]
@@ -105,6 +107,7 @@ def main():
     args = parse()
     import torch
     import torch.distributed as dist
+    import hcdist
     import hcodec as hc
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,7 +161,6 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
 
@@ -166,13 +168,18 @@ def main():
     bad = int((est != 0).sum() + (bst != 0).sum() + (blens != lens).sum())
     bad += 0 if torch.equal(back, raw) else 1
     enc_bytes = int(elens.sum())
-    counters = torch.tensor([bad, enc_bytes], dtype=torch.int64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        sizes = [torch.zeros_like(elens) for _ in range(world)]
-        dist.all_gather(sizes, elens)  # encoded size of every stream of the job, on every rank
-    bad, enc_total = int(counters[0]), int(counters[1])
+    elapsed = hcdist.reduce_counters([t1 - t0], op="max", device=dev)
+    bad, enc_total = (int(v) for v in hcdist.reduce_counters([bad, enc_bytes], device=dev))
+    sizes = hcdist.gather_sizes(elens)  # every stream's encoded size, on every rank
+    gather_ms = None
+    if args.gather:  # the encoded payloads of all ranks into rank 0 (RCCL all-gather)
+        torch.cuda.synchronize(dev)
+        g0 = time.perf_counter()
+        packed, _ = hcdist.gather_encoded(enc, eoffs, elens)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+        if rank == 0 and packed.numel() != int(sizes.sum()):
+            bad += 1
     if bad:
         raise SystemExit(f"bit-exact check FAILED on {bad} items")
 
@@ -207,7 +214,10 @@ def main():
         "encode_GiBps": round(world * S * N_RAW / (enc_ms * 1e-3) / 2**30, 4),
         "decode_GiBps": round(world * S * N_RAW / (dec_ms * 1e-3) / 2**30, 4),
         "bits_per_byte": round(enc_total * 8 / raw_total, 4), "bit_exact": True,
+        "streams_total": int(sizes.numel()),
     }
+    if gather_ms is not None:
+        result["gather_ms"] = round(gather_ms, 3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(args, cores)

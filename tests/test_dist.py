@@ -1,0 +1,91 @@
+"""Multi-process path on CPU (gloo, world size 2): stream sharding, counter reduction, size
+all-gather and the payload gather into rank 0 reproduce the single-process result exactly.
+The encoder here is the oracle (CPU checker) standing in for each rank's GPU encode — the
+point is the distributed bookkeeping, which is device-independent."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+W, H, PER_RANK = 48, 40, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _encode_shard(rank, world):
+    import oracle
+    import hcdist
+    blobs = []
+    for k in hcdist.shard(rank, world, PER_RANK):
+        st, out = oracle.compress(oracle.synth("photo", k, W, H).tobytes(), True, False, 512)
+        assert st == 0
+        blobs.append(out)
+    cap = max(len(b) for b in blobs) + 16
+    buf = torch.zeros(PER_RANK * cap, dtype=torch.uint8)
+    for i, b in enumerate(blobs):
+        buf[i * cap:i * cap + len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+    offs = torch.arange(PER_RANK, dtype=torch.int64) * cap
+    lens = torch.tensor([len(b) for b in blobs], dtype=torch.int64)
+    return buf, offs, lens
+
+
+def _worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "huffman-codec_amd", "python"), os.path.join(root, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import hcdist
+    buf, offs, lens = _encode_shard(rank, world)
+    total = hcdist.reduce_counters([int(lens.sum()), rank + 1])
+    mx = hcdist.reduce_counters([float(rank)], op="max")
+    packed, sizes = hcdist.gather_encoded(buf, offs, lens)
+    q.put((rank, total.tolist(), mx.tolist(), sizes.tolist(), None if packed is None else packed.numpy().tobytes()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gather_matches_single_process(oracle_mod):
+    import hcdist
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference of the same 6 streams
+    want = []
+    for k in range(world * PER_RANK):
+        want.append(oracle_mod.compress(oracle_mod.synth("photo", k, W, H).tobytes(), True, False, 512)[1])
+    for r in range(world):
+        assert res[r][1] == [sum(map(len, want)), 3]
+        assert res[r][2] == [1.0]
+        assert res[r][3] == [len(b) for b in want]
+    assert res[0][4] == b"".join(want)
+    assert res[1][4] is None
+    assert list(hcdist.shard(1, 2, 3)) == [3, 4, 5]
+
+
+def test_pack_single_process():
+    import hcdist
+    buf = torch.arange(40, dtype=torch.int64).to(torch.uint8)
+    offs = torch.tensor([0, 10, 30])
+    lens = torch.tensor([3, 0, 5])
+    assert hcdist.pack(buf, offs, lens).tolist() == [0, 1, 2, 30, 31, 32, 33, 34]
