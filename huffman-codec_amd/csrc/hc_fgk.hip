@@ -43,6 +43,7 @@ struct alignas(16) Tree {
     uint16_t body[516];               // symbol | kInner + child pair | kNyt
     uint16_t where[256];              // symbol -> position, 0 = not yet transmitted
     uint16_t up[kWide ? 516 : 8];     // wide: parent position
+    uint32_t syms[128];               // encoder: MNP-5 symbols of one 256-byte chunk (<= 512)
 };
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -248,6 +249,98 @@ struct Fgk {
     }
 };
 
+// -------------------------------------------------------------- MNP-5 pre-pass (encoder) --
+
+// Carry between chunks: last raw byte (diff model), run counter after the last byte (0 = no
+// run: stream start or a 258-byte cut), last transformed byte.
+struct RleCarry {
+    uint32_t x, R, c;
+};
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t b) { return (w >> (8 * b)) & 255u; }
+
+// transform.cpp:220-229 + 241-279 for one chunk, all lanes at once (model and derivation:
+// tests/rle_chunk_model.py). Lane l holds raw bytes 4l..4l+3 of the chunk in x4, m (1..256) are
+// valid, fin says byte m-1 is the stream's last. Per byte: k = offset in its run (the run may
+// continue from the previous chunk), km = k mod 258, run counter R = km + 1 (0 at the cut);
+// a byte emits the previous run's count byte and itself when a run starts (or it is the final
+// byte), itself at km 1..2, 255 at km 257, nothing otherwise. Symbols go to syms[] in order;
+// returns how many.
+template <int kSrc>
+__device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t fin, RleCarry &cy,
+                                              uint32_t *syms, uint32_t *scr, uint32_t lane)
+{
+    const uint32_t up = __shfl_up(x4, 1, 64);
+    const uint32_t xprev = (x4 << 8) | ((lane == 0 ? (cy.x << 24) : up) >> 24);
+    // bytewise x - xprev (mod 256), SWAR
+    const uint32_t c4 = kSrc == SRC_RAW_DIFF
+                            ? (((x4 | 0x80808080u) - (xprev & 0x7F7F7F7Fu)) ^ ((x4 ^ ~xprev) & 0x80808080u))
+                            : x4;
+    const uint32_t upc = __shfl_up(c4, 1, 64);
+    const uint32_t cprev = (c4 << 8) | ((lane == 0 ? (cy.c << 24) : upc) >> 24);
+    const int i0 = (int)(lane * 4);
+    uint32_t start[4], any = 0;
+    int last = -1;
+    for (uint32_t b = 0; b < 4; ++b) {
+        uint32_t same = byte_of(c4, b) == byte_of(cprev, b);
+        if (b == 0) same &= lane != 0 || cy.R != 0;  // lane 0 byte 0: continues the carry's run?
+        start[b] = (uint32_t)(i0 + (int)b < (int)m) & (same ^ 1u);
+        any |= start[b];
+        last = start[b] ? i0 + (int)b : last;
+    }
+    // latest run start in the lanes below (else the carried run, begun at -R)
+    const uint64_t amask = ballot(any != 0) & ((1ull << lane) - 1ull);
+    const int src = amask ? 63 - __builtin_clzll(amask) : 0;
+    const int below = __builtin_amdgcn_ds_bpermute(src * 4, last);
+    int ls = amask ? below : -(int)cy.R;
+    uint32_t R[4], km[4];
+    for (uint32_t b = 0; b < 4; ++b) {
+        ls = start[b] ? i0 + (int)b : ls;
+        const uint32_t k = (uint32_t)(i0 + (int)b - ls);
+        km[b] = k >= 258 ? k - 258 : k;
+        R[b] = km[b] == 257 ? 0u : km[b] + 1;
+    }
+    const uint32_t upR = __shfl_up(R[3], 1, 64);
+    uint32_t n[4], s0[4], s1[4], tot = 0;
+    for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t i = (uint32_t)i0 + b;
+        const uint32_t rp = b ? R[b - 1] : (lane == 0 ? cy.R : upR);
+        const uint32_t c = byte_of(c4, b);
+        const uint32_t valid = i < m ? 1u : 0u;
+        const uint32_t newrun = ((fin & (i + 1 == m ? 1u : 0u)) | (km[b] == 0 ? 1u : 0u));
+        const uint32_t cnt = newrun & (rp >= 3 ? 1u : 0u);
+        const uint32_t lit = km[b] == 1 || km[b] == 2 ? 1u : 0u;
+        const uint32_t cut = km[b] == 257 && !newrun ? 1u : 0u;
+        n[b] = valid * (newrun ? 1 + cnt : (lit | cut));
+        s0[b] = cnt ? rp - 3 : (cut ? 255u : c);
+        s1[b] = c;
+        tot += n[b];
+    }
+    // exclusive prefix of the per-lane totals (<= 8): bit planes, ballot + mbcnt
+    uint32_t basepos = 0;
+    for (uint32_t p = 0; p < 4; ++p) {
+        const uint64_t bm = ballot((tot >> p) & 1u);
+        basepos += __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << p;
+    }
+    uint8_t *sb = reinterpret_cast<uint8_t *>(syms);
+    uint8_t *sc = reinterpret_cast<uint8_t *>(scr);
+    uint32_t o = basepos;
+    for (uint32_t b = 0; b < 4; ++b) {
+        *(n[b] >= 1 ? sb + o : sc) = (uint8_t)s0[b];
+        *(n[b] == 2 ? sb + o + 1 : sc + 1) = (uint8_t)s1[b];
+        o += n[b];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = lane_read(basepos + tot, 63);
+    // carries: the chunk's last byte
+    const uint32_t L = m - 1, ll = L >> 2, lb = L & 3u;
+    const uint32_t rl = lb == 0 ? R[0] : (lb == 1 ? R[1] : (lb == 2 ? R[2] : R[3]));
+    cy.x = byte_of(lane_read(x4, ll), lb);
+    cy.c = byte_of(lane_read(c4, ll), lb);
+    cy.R = lane_read(rl, ll);
+    return total;
+}
+
 // ------------------------------------------------------------------------- output stage --
 
 // Bits gather in a scalar accumulator and leave as big-endian dwords through a VGPR stage of
@@ -366,44 +459,28 @@ __global__ __launch_bounds__(256) void encode_kernel(Batch bt)
         ++nsym;
     };
 
-    // transform.cpp:220-229 (diff) then transform.cpp:241-279 (MNP-5 RLE). run_byte = 0x100
-    // ("no run": at the start and after a 258-byte cut) folds the reference's run != 0 test
-    // into the byte compare; set right before the stream's final byte, it also sends that byte
-    // down the literal path as transform.cpp:252 does.
-    uint32_t prev = 0, run_byte = 0x100, run = 0;
     uint32_t next = buf_load(rin, lane * 4);
+    RleCarry cy = {0, 0, 0};
     for (uint32_t base = 0; base < n32 && !fgk.bad; base += 256) {
         const uint32_t chunk = next;
         next = buf_load(rin, base + 256 + lane * 4);  // out of range past the end: reads 0
         const uint32_t m = min(256u, n32 - base);
-        const uint32_t fin = base + m == n32 ? m - 1 : ~0u;  // index of the final byte, if here
+        if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
+            uint32_t word = 0;
+            for (uint32_t j = 0; j < m && !fgk.bad; ++j) {
+                if ((j & 3u) == 0) word = lane_read(chunk, j >> 2);
+                code((word >> (8 * (j & 3u))) & 255u);
+            }
+            continue;
+        }
+        // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
+        const uint32_t ns = rle_chunk<kSrc>(chunk, m, base + m == n32 ? 1u : 0u, cy, fgk.T.syms,
+                                            fgk.scr32(), lane);
+        const uint32_t lo = fgk.T.syms[lane], hi = fgk.T.syms[64 + lane];
         uint32_t word = 0;
-        for (uint32_t j = 0; j < m && !fgk.bad; ++j) {
-            if ((j & 3u) == 0) word = lane_read(chunk, j >> 2);
-            const uint32_t x = (word >> (8 * (j & 3u))) & 255u;
-            if (kSrc == SRC_SYMBOLS) {
-                code(x);
-                continue;
-            }
-            const uint32_t c = kSrc == SRC_RAW_DIFF ? ((x - prev) & 255u) : x;
-            prev = x;
-            if (j == fin) run_byte = 0x100;
-            uint32_t q, nq;  // up to two symbols, first in the low byte
-            if (c == run_byte) {
-                ++run;
-                const uint32_t cut = run == 258 ? 1u : 0u;  // 255 + 3
-                nq = (run <= 3 ? 1u : 0u) | cut;
-                q = cut ? 255u : c;
-                run = cut ? 0u : run;
-                run_byte = cut ? 0x100u : run_byte;
-            } else {
-                const uint32_t cnt = run >= 3 ? 1u : 0u;
-                nq = 1 + cnt;
-                q = cnt ? ((run - 3) | (c << 8)) : c;
-                run_byte = c;
-                run = 1;
-            }
-            for (; nq; --nq, q >>= 8) code(q & 255u);
+        for (uint32_t t = 0; t < ns && !fgk.bad; ++t) {
+            if ((t & 3u) == 0) word = lane_read(t < 256 ? lo : hi, (t >> 2) & 63u);
+            code((word >> (8 * (t & 3u))) & 255u);
         }
     }
 
