@@ -62,6 +62,14 @@ __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// A wave-uniform value held in a VGPR: hiding its uniformity from the compiler moves the
+// arithmetic on it from the (saturated) scalar unit to the vector ALUs. Branches on such
+// values go through ballot(), which is uniform again.
+__device__ __forceinline__ uint32_t vreg(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
 
 // range-checked view of one stream's bytes; the arguments must be wave-uniform
 __device__ __forceinline__ rsrc_t make_rsrc(const uint8_t *p, uint32_t bytes)
@@ -172,16 +180,20 @@ struct Fgk {
 
     // Encoder: the path from position s to the root, BEFORE the update (the code of
     // huffman.cpp:136-155): the position of level k (0 = s) goes to lane k; returns the levels.
-    __device__ __forceinline__ uint32_t chase(uint32_t s, uint32_t &pv)
+    __device__ __forceinline__ uint32_t chase(uint32_t s0, uint32_t &pv)
     {
         uint32_t k = 0;
+        uint32_t s = vreg(s0);  // per-level work on the VALU (see vreg)
         pv = kRoot + 1;
-        do {
+        for (;;) {
             pv = lane == k ? s : pv;
             ++k;
-            s = max(parent(s), s + 1);  // parents sit above children; max() bounds a bug
-        } while (s < kRoot);
-        bad |= (s ^ kRoot) | (k > 64 ? 1u : 0u);
+            const uint32_t p = kWide ? (uint32_t)T.up[s] : (T.wt[s] & 1023u);
+            s = max(p, s + 1);  // parents sit above children; max() bounds a bug
+            if (!ballot(s < kRoot)) break;
+        }
+        bad |= uni(s) ^ kRoot;
+        bad |= k > 64 ? 1u : 0u;
         return k;
     }
 
