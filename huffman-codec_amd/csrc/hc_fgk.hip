@@ -36,14 +36,31 @@ constexpr int kWaves = 4;
 constexpr uint32_t kMaxBufBytes = 0x7FFFFF00u;  // per-stream limit of the 32-bit buffer offsets
 constexpr uint32_t kDrop = 0x7FFFFFF8u;         // buffer offset past every range: access dropped
 
-template <bool kWide>
+constexpr uint32_t kSlots = 8;      // encoder path cache: entries
+constexpr uint32_t kSlotDepth = 16; // deepest cached path (its code bits fit 16 bits)
+constexpr uint32_t kRefresh = 16;   // decoder: rebuild the level tables after this many lookups
+                                    // they left short of depth 8
+constexpr uint32_t kMarkShift = 10; // decoder: body bits 10..15 = table generation (per position)
+
+// One wavefront's LDS; <= 5 KB so that 8 four-wave workgroups fit a CU. Encoder and decoder
+// each add their cache (tests/fgk_cache_model.py is the executable model of both, checked
+// against the plain slot form).
+template <bool kWide, bool kDec>
 struct alignas(16) Tree {
     uint32_t wt[kWords];              // narrow: weight << 10 | parent; wide: weight
     uint32_t scratch[64];             // landing words of lanes that must not write
-    uint16_t body[516];               // symbol | kInner + child pair | kNyt
-    uint16_t where[256];              // symbol -> position, 0 = not yet transmitted
-    uint16_t up[kWide ? 516 : 8];     // wide: parent position
-    uint32_t syms[128];               // encoder: MNP-5 symbols of one 256-byte chunk (<= 512)
+    // encoder path cache entry e: code bits | depth << 16 | valid << 21 | symbol << 24
+    uint32_t pc_meta[kDec ? 1 : kSlots];
+    // symbol | kInner + child pair | kNyt; decoder: bits 10..15 = generation of the level
+    // tables that walked through this position
+    uint16_t body[516];
+    uint16_t where[kDec ? 2 : 256];   // encoder: symbol -> position | (entry + 1) << 10; 0 = unseen
+    uint16_t up[kWide ? 516 : 2];     // wide: parent position
+    alignas(8) uint32_t syms[kDec ? 1 : 128];  // encoder: MNP-5 symbols of one 256-byte chunk
+    alignas(8) uint16_t pc_pos[kDec ? 2 : kSlots * kSlotDepth];  // [entry][level] positions
+    // decoder level tables: level j (1..8) at 2^j - 2 + prefix: position | depth << 10 where
+    // the walk from the root along the prefix's bits stops
+    uint16_t lvl[kDec ? 512 : 2];
 };
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -91,17 +108,22 @@ __device__ __forceinline__ void buf_store8(rsrc_t r, uint32_t off, uint32_t v)
 
 // ------------------------------------------------------------------------------ the tree --
 
-template <bool kWide>
+template <bool kWide, bool kDec>
 struct Fgk {
     static constexpr uint32_t kInc = kWide ? 1u : 1024u;
 
-    Tree<kWide> &T;
+    Tree<kWide, kDec> &T;
     uint32_t lane;
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
     uint32_t rootw;  // the root's word (weight = symbols coded so far)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
+    uint32_t pc_next;  // encoder: next cache entry to fill (round robin)
+    uint32_t gen;      // decoder: generation of the level tables
+    uint32_t dirty;    // decoder: a swap moved a position the tables walk through
+    uint32_t shortc;   // decoder: lookups the tables left short since the last build
 
-    __device__ Fgk(Tree<kWide> &t, uint32_t l) : T(t), lane(l), nyt(kRoot), rootw(0), bad(0)
+    __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
+        : T(t), lane(l), nyt(kRoot), rootw(0), bad(0), pc_next(0), gen(0), dirty(1), shortc(0)
     {
         // huffman.cpp:23-31: a lone NYT root
         for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
@@ -109,7 +131,11 @@ struct Fgk {
             T.body[i] = i == kRoot ? kNyt : 0;
             if (kWide) T.up[i] = 0;
         }
-        for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
+        if (!kDec) {
+            for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
+            for (uint32_t i = lane; i < kSlots; i += 64) T.pc_meta[i] = 0;
+            for (uint32_t i = lane; i < kSlots * kSlotDepth; i += 64) T.pc_pos[i] = 0xFFFF;
+        }
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -118,6 +144,92 @@ struct Fgk {
     __device__ __forceinline__ uint16_t *scr16() const
     {
         return reinterpret_cast<uint16_t *>(&T.scratch[lane]);
+    }
+    __device__ __forceinline__ uint8_t *scr8() const { return reinterpret_cast<uint8_t *>(&T.scratch[lane]); }
+
+    // ---- encoder path cache: root paths of recently coded symbols (tests/fgk_cache_model.py).
+    // A path changes only when a swap moves a position on it; splits touch no symbol's path.
+
+    // hit: entry e's path to lanes 0..d-1 (kRoot + 1 above), its code bits; returns d
+    __device__ __forceinline__ uint32_t pc_get(uint32_t e, uint32_t &pv, uint32_t &bits) const
+    {
+        const uint32_t p = T.pc_pos[e * kSlotDepth + (lane & (kSlotDepth - 1))];
+        pv = lane < kSlotDepth ? p : kRoot + 1;
+        const uint32_t m = uni(T.pc_meta[e]);
+        bits = m & 0xFFFFu;
+        return (m >> 16) & 31u;
+    }
+
+    // forget entry e (its symbol's where[] keeps only the position: level 0 of the path)
+    __device__ __forceinline__ void pc_forget(uint32_t e, uint32_t lane0, uint16_t *other, uint32_t oval)
+    {
+        const uint32_t m = uni(T.pc_meta[e]);
+        const uint32_t opos = uni(T.pc_pos[e * kSlotDepth]);
+        uint16_t *q = lane == lane0 ? ((m >> 21) & 1u ? &T.where[m >> 24] : scr16()) : other;
+        *q = (uint16_t)(lane == lane0 ? opos : oval);
+    }
+
+    // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot + 1)
+    __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t bits)
+    {
+        if (d > kSlotDepth) return;
+        const uint32_t e = pc_next;
+        pc_next = (e + 1) & (kSlots - 1);
+        // lane 0: the evicted symbol forgets its entry; lane 1: this symbol takes it
+        pc_forget(e, 0, lane == 1 ? &T.where[sym] : scr16(), s | ((e + 1) << 10));
+        *(lane < kSlotDepth ? &T.pc_pos[e * kSlotDepth + lane] : scr16()) = (uint16_t)pv;
+        *(lane == 0 ? &T.pc_meta[e] : scr32()) = bits | (d << 16) | (1u << 21) | (sym << 24);
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    __device__ void pc_drop(uint32_t e)
+    {
+        pc_forget(e, 0, scr16(), 0);
+        *(lane < kSlotDepth ? &T.pc_pos[e * kSlotDepth + lane] : scr16()) = (uint16_t)0xFFFF;
+        *(lane == 0 ? &T.pc_meta[e] : scr32()) = 0u;
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // positions s and l traded contents: drop every cached path through either. Lane k reads
+    // levels 2(k&7), 2(k&7)+1 of entry k>>3; byte e of the ballot flags entry e.
+    __device__ __forceinline__ void pc_swapped(uint32_t s, uint32_t l)
+    {
+        const uint32_t q = reinterpret_cast<const uint32_t *>(T.pc_pos)[lane];
+        const uint32_t a = q ^ (s | (s << 16)), c = q ^ (l | (l << 16));
+        const uint32_t z = ((a & 0xFFFFu) == 0) | ((a >> 16) == 0) | ((c & 0xFFFFu) == 0) | ((c >> 16) == 0);
+        uint64_t m = ballot(z);
+        while (m) {
+            const uint32_t e = (uint32_t)__builtin_ctzll(m) >> 3;
+            m &= ~(0xFFull << (8 * e));
+            pc_drop(e);
+        }
+    }
+
+    // ---- decoder level tables (tests/fgk_cache_model.py: LevelTables). Level j's entry for a
+    // j-bit prefix is where the walk from the root along those bits stops (position | depth <<
+    // 10); built breadth first, each level from the one above. A swap stales them only when it
+    // moves the content of a position some walk passes through: those carry the generation.
+    __device__ void build_levels()
+    {
+        gen = gen == 63 ? 1u : gen + 1;
+#pragma unroll 1
+        for (uint32_t j = 1; j <= 8; ++j) {
+            const uint32_t cnt = 1u << j;
+            for (uint32_t r = 0; r * 64 < cnt; ++r) {
+                const uint32_t q = lane + 64 * r;
+                const bool on = q < cnt;
+                const uint32_t pe = j == 1 ? kRoot : T.lvl[(cnt >> 1) - 2 + (on ? q >> 1 : 0)];
+                const uint32_t x = pe & 1023u;
+                const uint32_t b = T.body[x];
+                const bool inner = (b & kInner) && (pe >> 10) == j - 1;
+                *(on && inner ? &T.body[x] : scr16()) = (uint16_t)((b & 0x3FFu) | (gen << kMarkShift));
+                const uint32_t ne = inner ? (((b & 255u) * 2 + (q & 1u)) | (j << 10)) : pe;
+                *(on ? &T.lvl[cnt - 2 + q] : scr16()) = (uint16_t)ne;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        dirty = 0;
+        shortc = 0;
     }
 
     // huffman.cpp:99-111: split NYT at t -> NYT at t-2 (left), symbol leaf at t-1 (right).
@@ -128,7 +240,7 @@ struct Fgk {
         const uint32_t bpos = lane == 0 ? t : (lane == 1 ? t - 2 : t - 1);
         const uint32_t bval = lane == 0 ? (kInner | ((t - 2) >> 1)) : (lane == 1 ? kNyt : sym);
         *(lane < 3 ? &T.body[bpos] : scr16()) = (uint16_t)bval;
-        *(lane == 0 ? &T.where[sym] : scr16()) = (uint16_t)(t - 1);
+        if (!kDec) *(lane == 0 ? &T.where[sym] : scr16()) = (uint16_t)(t - 1);
         if (kWide) *(lane < 2 ? &T.up[t - 2 + lane] : scr16()) = (uint16_t)t;
         else *(lane < 2 ? &T.wt[t - 2 + lane] : scr32()) = t;  // weight 0, parent t
         __builtin_amdgcn_wave_barrier();
@@ -141,13 +253,22 @@ struct Fgk {
     // moving into (k ? l : s); lane k < 4 re-parents child (k & 1) of content (k >> 1).
     __device__ __forceinline__ void swap(uint32_t s, uint32_t l)
     {
+        // encoder: drop the cached paths through s or l first; the relink below then gives a
+        // moved leaf's where[] its new position
+        if (!kDec) pc_swapped(s, l);
         const uint32_t bs = uni(T.body[s]);
         const uint32_t bl = uni(T.body[l]);
         const uint32_t k = lane >> 1;                 // 0: content going to s, 1: to l
-        const uint32_t b = (lane & 1) ? bs : bl;      // lanes 0/1: body for s / l
+        const uint32_t b = (lane & 1) ? bs : bl;      // lanes 0/1: content for s / l
         const uint32_t pos = (lane & 1) ? l : s;
-        *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
-        *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
+        if (kDec) {  // generation marks stay with the positions
+            const uint32_t keep = ((lane & 1) ? bl : bs) & ~0x3FFu;
+            *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & 0x3FFu) | keep);
+            dirty |= (uint32_t)((bs >> kMarkShift) == gen) | (uint32_t)((bl >> kMarkShift) == gen);
+        } else {
+            *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
+            *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
+        }
         const uint32_t cb = k ? bs : bl;              // lanes 0..3: content whose child moves
         const uint32_t cpos = k ? l : s;
         const bool inner = lane < 4 && (cb & kInner);
@@ -364,8 +485,8 @@ struct BitSink {
     uint32_t wbase;  // word index of stage lane 0
     uint32_t widx;   // next stage lane
     uint32_t stage;
-    uint64_t acc;
-    uint32_t nacc;
+    uint64_t acc;    // pending bits, MSB-aligned
+    uint32_t nacc;   // pending bit count, < 32 between calls
 
     __device__ __forceinline__ void word(uint32_t w)
     {
@@ -376,14 +497,15 @@ struct BitSink {
             widx = 0;
         }
     }
-    // append the n (<= 32) low bits of x, MSB first
+    // append the n (1..32) low bits of x, MSB first
     __device__ __forceinline__ void put(uint32_t x, uint32_t n)
     {
-        acc = (acc << n) | x;
+        acc |= (uint64_t)x << (64 - nacc - n);
         nacc += n;
         if (nacc >= 32) {
+            word((uint32_t)(acc >> 32));
+            acc <<= 32;
             nacc -= 32;
-            word((uint32_t)(acc >> nacc));
         }
     }
     __device__ __forceinline__ void put64(uint64_t x, uint32_t n)
@@ -400,7 +522,7 @@ struct BitSink {
     {
         if (nacc & 7u) put(0, 8 - (nacc & 7u));
         const uint32_t tail = nacc >> 3;  // 0..3 bytes pending
-        const uint32_t tw = tail ? (uint32_t)(acc << (32 - nacc)) : 0u;  // MSB-aligned
+        const uint32_t tw = (uint32_t)(acc >> 32);
         // whole words of the stage, then the tail bytes from lane widx
         buf_store(rs, lane < widx ? (wbase + lane) * 4 : kDrop, stage);
         const uint32_t tb = (wbase + widx) * 4;
@@ -413,9 +535,9 @@ struct BitSink {
 // --------------------------------------------------------------------------- the encoder --
 
 template <bool kWide, int kSrc>
-__global__ __launch_bounds__(256) void encode_kernel(Batch bt)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void encode_kernel(Batch bt)
 {
-    __shared__ Tree<kWide> trees[kWaves];
+    __shared__ Tree<kWide, false> trees[kWaves];
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
@@ -438,7 +560,7 @@ __global__ __launch_bounds__(256) void encode_kernel(Batch bt)
         return;
     }
 
-    Fgk<kWide> fgk(trees[wv], lane);
+    Fgk<kWide, false> fgk(trees[wv], lane);
     BitSink sink;
     sink.rs = make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
     sink.lane = lane;
@@ -450,27 +572,41 @@ __global__ __launch_bounds__(256) void encode_kernel(Batch bt)
     const uint32_t flags = kSrc == SRC_SYMBOLS ? bt.flags : (kSrc == SRC_RAW_DIFF ? 0x80u : 0u);
     sink.put(flags, 8);  // headers.cpp:118-122
 
-    uint64_t nsym = 0;
     const uint32_t n32 = (uint32_t)n;
     const rsrc_t rin = make_rsrc(bt.in + in_off, (n32 + 3u) & ~3u);
 
-    // transform.cpp:363-384: per symbol encode (path before update), then update
+    // transform.cpp:363-384: per symbol encode (path before update), then update. Positions
+    // stay in range by construction, so `bad` (a bug detector) is checked once per chunk.
     auto code = [&](uint32_t sym) {
-        uint32_t s = uni(fgk.T.where[sym]);
+        const uint32_t ws = uni(fgk.T.where[sym]);
+        uint32_t s = ws & 1023u;
+        if (ws >> 10) {  // path cached (never for a fresh symbol)
+            uint32_t pv, bits;
+            const uint32_t d = fgk.pc_get((ws >> 10) - 1, pv, bits);
+            fgk.update_path(pv, 0, d - 1);
+            sink.put(bits, d);
+            return;
+        }
         const uint32_t fresh = s == 0;
         if (fresh) s = uni(fgk.split(sym));
         uint32_t pv;
         const uint32_t d = fgk.chase(s, pv);
         // bit k = code bit (position parity, left = even) of level k; read MSB first it is the
-        // root-to-leaf code. A fresh symbol starts at its new leaf, one level below the NYT
-        // whose code is sent (huffman.cpp:44-50), so that lowest bit is dropped.
+        // root-to-leaf code
         const uint64_t bits = ballot((pv & 1u) && lane < d);
+        fgk.pc_insert(sym, s, pv, d, (uint32_t)bits);
         fgk.update_path(pv, 0, d - 1);
-        if (d > fresh) sink.put64(bits >> fresh, d - fresh);
-        if (fresh) sink.put(sym, 8);  // NYT code + 8 raw bits
-        ++nsym;
+        if (fresh) {
+            // the path starts at the new leaf, one level below the NYT whose code is sent
+            // (huffman.cpp:44-50): drop that lowest bit, then 8 raw bits
+            if (d > 1) sink.put64(bits >> 1, d - 1);
+            sink.put(sym, 8);
+        } else {
+            sink.put64(bits, d);
+        }
     };
 
+    uint64_t nsym = 0;
     uint32_t next = buf_load(rin, lane * 4);
     RleCarry cy = {0, 0, 0};
     for (uint32_t base = 0; base < n32 && !fgk.bad; base += 256) {
@@ -479,10 +615,11 @@ __global__ __launch_bounds__(256) void encode_kernel(Batch bt)
         const uint32_t m = min(256u, n32 - base);
         if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
             uint32_t word = 0;
-            for (uint32_t j = 0; j < m && !fgk.bad; ++j) {
+            for (uint32_t j = 0; j < m; ++j) {
                 if ((j & 3u) == 0) word = lane_read(chunk, j >> 2);
                 code((word >> (8 * (j & 3u))) & 255u);
             }
+            nsym += m;
             continue;
         }
         // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
@@ -490,10 +627,11 @@ __global__ __launch_bounds__(256) void encode_kernel(Batch bt)
                                             fgk.scr32(), lane);
         const uint32_t lo = fgk.T.syms[lane], hi = fgk.T.syms[64 + lane];
         uint32_t word = 0;
-        for (uint32_t t = 0; t < ns && !fgk.bad; ++t) {
+        for (uint32_t t = 0; t < ns; ++t) {
             if ((t & 3u) == 0) word = lane_read(t < 256 ? lo : hi, (t >> 2) & 63u);
             code((word >> (8 * (t & 3u))) & 255u);
         }
+        nsym += ns;
     }
 
     const uint64_t total = sink.finish();
@@ -581,9 +719,9 @@ struct ByteSink {
 };
 
 template <bool kWide, int kDst>
-__global__ __launch_bounds__(256) void decode_kernel(Batch bt)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void decode_kernel(Batch bt)
 {
-    __shared__ Tree<kWide> trees[kWaves];
+    __shared__ Tree<kWide, true> trees[kWaves];
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
@@ -620,7 +758,7 @@ __global__ __launch_bounds__(256) void decode_kernel(Batch bt)
         return;
     }
 
-    Fgk<kWide> fgk(trees[wv], lane);
+    Fgk<kWide, true> fgk(trees[wv], lane);
     BitSource in;
     in.rs = rin;
     in.lane = lane;
@@ -632,7 +770,6 @@ __global__ __launch_bounds__(256) void decode_kernel(Batch bt)
     in.refill();  // word 2: flags byte + first payload bits
     in.win <<= 8;
     in.nwin -= 8;
-    uint64_t left = (len - 9) * 8;  // payload bits not consumed yet
 
     ByteSink out;
     out.rs = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
@@ -641,80 +778,97 @@ __global__ __launch_bounds__(256) void decode_kernel(Batch bt)
     out.cur = 0;
     out.stage = 0;
 
-    const uint32_t diff = kDst == DST_RAW && (flags & 0x80u);
+    const uint32_t dmask = kDst == DST_RAW && (flags & 0x80u) ? 255u : 0u;  // diff model
     uint32_t prev = 0, run_byte = 0, run = 0;
     const uint32_t n = (uint32_t)count;
+    // bits read from the stream = words pushed into the window * 32 - bits still in it; the
+    // payload starts at bit 72. A stream that ends early decodes zero bits past its end (the
+    // range check); the reference stops there with status 9 (transform.cpp:394-398), which is
+    // what the comparison after the loop reports.
+    const uint64_t payload_bits = (len - 9) * 8;
+    auto consumed = [&]() -> uint64_t {
+        return (uint64_t)(in.cbase / 4 + in.ridx) * 32 - in.nwin - 72;
+    };
 
-    for (uint32_t i = 0; i < n; ++i) {
-        // huffman.cpp:60-93: walk down from the root over a window of >= 33 bits; the visited
-        // positions go to lanes 63, 62, ... so that lanes lo..63 hold the path bottom-up
-        if (in.nwin <= 32) in.refill();
-        uint32_t x = kRoot, depth = 0, pv = kRoot + 1;
-        uint64_t w = in.win;
-        uint32_t b = uni(fgk.T.body[kRoot]);
-        while (b & kInner) {
-            x = min((b & 255u) * 2 + (uint32_t)(w >> 63), x - 1);  // children sit below
-            w <<= 1;
-            pv = lane == 63 - depth ? x : pv;
-            ++depth;
-            b = uni(fgk.T.body[x]);
-        }
-        if (depth <= in.nwin) {
-            in.win = w;
-            in.nwin -= depth;
-        } else {  // a code longer than the window (deep trees only): again, bit by bit
-            x = kRoot;
-            depth = 0;
-            pv = kRoot + 1;
-            b = uni(fgk.T.body[kRoot]);
-            while (b & kInner) {
-                x = min((b & 255u) * 2 + in.bit(), x - 1);
+    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+        if (fgk.bad || out.pos > kMaxBufBytes || consumed() > payload_bits + 64) break;
+        const uint32_t i1 = min(n, i0 + 256);
+        for (uint32_t i = i0; i < i1; ++i) {
+            // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
+            // where the walk from the root stops, lane 64-j reads level j's position for the
+            // same prefix, so lanes lo..63 hold the path bottom-up. Codes longer than the
+            // tables reach go on from there bit by bit over a window of >= 33 bits.
+            if (fgk.dirty | (uint32_t)(fgk.shortc >= kRefresh)) fgk.build_levels();
+            if (in.nwin <= 32) in.refill();
+            const uint32_t v = (uint32_t)(in.win >> 56);
+            const uint32_t e8 = uni(fgk.T.lvl[254 + v]);
+            uint32_t x = e8 & 1023u, depth = e8 >> 10;
+            const uint32_t jl = 64 - lane, jc = jl > 8 ? 8 : jl;
+            uint32_t pv = fgk.T.lvl[(1u << jc) - 2 + (v >> (8 - jc))] & 1023u;
+            pv = jl <= depth ? pv : kRoot + 1;
+            uint32_t b = uni(fgk.T.body[x]);
+            if (b & kInner) {
+                fgk.shortc += depth < 8 ? 1u : 0u;
+                uint64_t w = in.win << depth;
+                do {
+                    x = min((b & 255u) * 2 + (uint32_t)(w >> 63), x - 1);  // children sit below
+                    w <<= 1;
+                    pv = lane == 63 - depth ? x : pv;
+                    ++depth;
+                    b = uni(fgk.T.body[x]);
+                } while (b & kInner);
+                if (depth > in.nwin) {  // a code longer than the window (deep trees only)
+                    x = kRoot;
+                    depth = 0;
+                    pv = kRoot + 1;
+                    b = uni(fgk.T.body[kRoot]);
+                    while (b & kInner) {
+                        x = min((b & 255u) * 2 + in.bit(), x - 1);
+                        pv = lane == 63 - depth ? x : pv;
+                        ++depth;
+                        b = uni(fgk.T.body[x]);
+                    }
+                } else {
+                    in.win = w;
+                    in.nwin -= depth;
+                }
+                if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
+            } else {
+                in.win <<= depth;
+                in.nwin -= depth;
+            }
+            uint32_t sym;
+            if (b & kNyt) {
+                sym = in.bits8();
+                x = uni(fgk.split(sym));
                 pv = lane == 63 - depth ? x : pv;
                 ++depth;
-                b = uni(fgk.T.body[x]);
+            } else {
+                sym = b & 255u;
             }
-        }
-        uint32_t sym, used = depth;
-        if (b & kNyt) {
-            sym = in.bits8();
-            used += 8;
-            x = uni(fgk.split(sym));
-            pv = lane == 63 - depth ? x : pv;
-            ++depth;
-        } else {
-            sym = b & 255u;
-        }
-        if (used > left) {  // ran past the payload: transform.cpp:394-398
-            st = HC_ERR_HUFFMAN;
-            break;
-        }
-        left -= used;
-        if (depth > 63) fgk.bad = 1;
-        fgk.update_path(pv, 64 - depth, 63);
-        if (fgk.bad) break;
+            fgk.update_path(pv, 64 - depth, 63);
 
-        if (kDst == DST_SYMBOLS) {
-            out.byte(sym);
-            continue;
-        }
-        // transform.cpp:137-159 (RLE revert), then transform.cpp:231-239 (diff revert)
-        if (run == 3) {
-            for (uint32_t r = 0; r < sym; ++r) {
-                prev = diff ? ((prev + run_byte) & 255u) : run_byte;
-                out.byte(prev);
+            if (kDst == DST_SYMBOLS) {
+                out.byte(sym);
+                continue;
             }
-            run = 0;
-        } else {
-            prev = diff ? ((prev + sym) & 255u) : sym;
-            out.byte(prev);
-            run = sym == run_byte ? run + 1 : 1;
-            run_byte = sym;
-        }
-        if (out.pos > kMaxBufBytes) {  // beyond the 32-bit buffer offsets of the device path
-            st = HC_ERR_UNSUPPORTED;
-            break;
+            // transform.cpp:137-159 (RLE revert), then transform.cpp:231-239 (diff revert)
+            if (run == 3) {
+                for (uint32_t r = 0; r < sym; ++r) {
+                    prev = ((prev & dmask) + run_byte) & 255u;
+                    out.byte(prev);
+                }
+                run = 0;
+            } else {
+                prev = ((prev & dmask) + sym) & 255u;
+                out.byte(prev);
+                run = sym == run_byte ? run + 1 : 1;
+                run_byte = sym;
+            }
         }
     }
+    if (consumed() > payload_bits) st = HC_ERR_HUFFMAN;  // ran past the payload
+    else if (out.pos > kMaxBufBytes) st = HC_ERR_UNSUPPORTED;  // beyond the device path's offsets
     if (fgk.bad) st = HC_ERR_DEVICE;
     if (st == 0) out.finish();
     if (st == 0 && out.pos > cap) st = HC_ERR_CAPACITY;

@@ -5,12 +5,17 @@ tag = sys.argv[1]
 syms = float(sys.argv[2]) if len(sys.argv) > 2 else 8192 * 201635
 base = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'gpurun_out', 'prof')
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
+launches = collections.defaultdict(set)  # per (kernel, pass): dispatches, to report per launch
 for f in glob.glob(os.path.join(base, f'{tag}_pmc_*', '*counter_collection.csv')):
     for r in csv.DictReader(open(f)):
         k = r['Kernel_Name']
         if 'encode_kernel<false' in k or 'decode_kernel<false' in k:
-            agg[('encode' if 'encode_kernel' in k else 'decode')][r['Counter_Name']] += float(r['Counter_Value'])
+            kk = 'encode' if 'encode_kernel' in k else 'decode'
+            agg[kk][r['Counter_Name']] += float(r['Counter_Value'])
+            launches[(kk, r['Counter_Name'])].add(r['Dispatch_Id'])
 for k, d in agg.items():
+    for c in d:
+        d[c] /= max(1, len(launches[(k, c)]))
     cyc = d.get('GRBM_GUI_ACTIVE', 0) / 8
     print(k, f"cycles/XCD {cyc:.3g}")
     for c in ('SQ_INSTS_SALU', 'SQ_INSTS_VALU', 'SQ_INSTS_LDS'):
