@@ -38,6 +38,7 @@ constexpr uint32_t kDrop = 0x7FFFFFF8u;         // buffer offset past every rang
 
 constexpr uint32_t kSlots = 8;      // encoder path cache: entries
 constexpr uint32_t kSlotDepth = 16; // deepest cached path (its code bits fit 16 bits)
+constexpr uint32_t kRow = 20;       // u16 per cache entry
 constexpr uint32_t kRefresh = 16;   // decoder: rebuild the level tables after this many lookups
                                     // they left short of depth 8
 constexpr uint32_t kMarkShift = 10; // decoder: body bits 10..15 = table generation (per position)
@@ -49,15 +50,16 @@ template <bool kWide, bool kDec>
 struct alignas(16) Tree {
     uint32_t wt[kWords];              // narrow: weight << 10 | parent; wide: weight
     uint32_t scratch[64];             // landing words of lanes that must not write
-    // encoder path cache entry e: code bits | depth << 16 | valid << 21 | symbol << 24
-    uint32_t pc_meta[kDec ? 1 : kSlots];
     // symbol | kInner + child pair | kNyt; decoder: bits 10..15 = generation of the level
     // tables that walked through this position
     uint16_t body[516];
     uint16_t where[kDec ? 2 : 256];   // encoder: symbol -> position | (entry + 1) << 10; 0 = unseen
     uint16_t up[kWide ? 516 : 2];     // wide: parent position
     alignas(8) uint32_t syms[kDec ? 1 : 128];  // encoder: MNP-5 symbols of one 256-byte chunk
-    alignas(8) uint16_t pc_pos[kDec ? 2 : kSlots * kSlotDepth];  // [entry][level] positions
+    // encoder path cache, entry e = row e: positions of levels 0..15 (kRoot above the path),
+    // [16] code bits, [17] depth | valid << 5 | symbol << 8, [18..19] unused. One lane-based
+    // address reads a lane's position and (lane 0) the row's metadata.
+    alignas(8) uint16_t pc[kDec ? 2 : kSlots * kRow];
     // decoder level tables: level j (1..8) at 2^j - 2 + prefix: position | depth << 10 where
     // the walk from the root along the prefix's bits stops
     uint16_t lvl[kDec ? 512 : 2];
@@ -115,7 +117,6 @@ struct Fgk {
     Tree<kWide, kDec> &T;
     uint32_t lane;
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
-    uint32_t rootw;  // the root's word (weight = symbols coded so far)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
     uint32_t pc_next;  // encoder: next cache entry to fill (round robin)
     uint32_t gen;      // decoder: generation of the level tables
@@ -123,7 +124,7 @@ struct Fgk {
     uint32_t shortc;   // decoder: lookups the tables left short since the last build
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
-        : T(t), lane(l), nyt(kRoot), rootw(0), bad(0), pc_next(0), gen(0), dirty(1), shortc(0)
+        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), gen(0), dirty(1), shortc(0)
     {
         // huffman.cpp:23-31: a lone NYT root
         for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
@@ -133,8 +134,7 @@ struct Fgk {
         }
         if (!kDec) {
             for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
-            for (uint32_t i = lane; i < kSlots; i += 64) T.pc_meta[i] = 0;
-            for (uint32_t i = lane; i < kSlots * kSlotDepth; i += 64) T.pc_pos[i] = 0xFFFF;
+            for (uint32_t i = lane; i < kSlots * kRow; i += 64) T.pc[i] = (i % kRow) < kSlotDepth ? 0xFFFF : 0;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -150,26 +150,25 @@ struct Fgk {
     // ---- encoder path cache: root paths of recently coded symbols (tests/fgk_cache_model.py).
     // A path changes only when a swap moves a position on it; splits touch no symbol's path.
 
-    // hit: entry e's path to lanes 0..d-1 (kRoot + 1 above), its code bits; returns d
+    // hit: entry e's path to lanes 0..d-1 (kRoot above), its code bits; returns d
     __device__ __forceinline__ uint32_t pc_get(uint32_t e, uint32_t &pv, uint32_t &bits) const
     {
-        const uint32_t p = T.pc_pos[e * kSlotDepth + (lane & (kSlotDepth - 1))];
-        pv = lane < kSlotDepth ? p : kRoot + 1;
-        const uint32_t m = uni(T.pc_meta[e]);
-        bits = m & 0xFFFFu;
-        return (m >> 16) & 31u;
+        const uint16_t *row = &T.pc[e * kRow] + (lane & (kSlotDepth - 1));  // lane 0: row start
+        pv = lane < kSlotDepth ? (uint32_t)row[0] : kRoot;
+        bits = uni(row[16]);
+        return uni(row[17]) & 31u;
     }
 
     // forget entry e (its symbol's where[] keeps only the position: level 0 of the path)
     __device__ __forceinline__ void pc_forget(uint32_t e, uint32_t lane0, uint16_t *other, uint32_t oval)
     {
-        const uint32_t m = uni(T.pc_meta[e]);
-        const uint32_t opos = uni(T.pc_pos[e * kSlotDepth]);
-        uint16_t *q = lane == lane0 ? ((m >> 21) & 1u ? &T.where[m >> 24] : scr16()) : other;
+        const uint32_t m = uni(T.pc[e * kRow + 17]);
+        const uint32_t opos = uni(T.pc[e * kRow]);
+        uint16_t *q = lane == lane0 ? ((m >> 5) & 1u ? &T.where[m >> 8] : scr16()) : other;
         *q = (uint16_t)(lane == lane0 ? opos : oval);
     }
 
-    // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot + 1)
+    // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot)
     __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t bits)
     {
         if (d > kSlotDepth) return;
@@ -177,16 +176,16 @@ struct Fgk {
         pc_next = (e + 1) & (kSlots - 1);
         // lane 0: the evicted symbol forgets its entry; lane 1: this symbol takes it
         pc_forget(e, 0, lane == 1 ? &T.where[sym] : scr16(), s | ((e + 1) << 10));
-        *(lane < kSlotDepth ? &T.pc_pos[e * kSlotDepth + lane] : scr16()) = (uint16_t)pv;
-        *(lane == 0 ? &T.pc_meta[e] : scr32()) = bits | (d << 16) | (1u << 21) | (sym << 24);
+        // lanes 0..15 the positions, 16 the code bits, 17 depth | valid | symbol
+        const uint32_t rv = lane < kSlotDepth ? pv : (lane == 16 ? bits : (d | 32u | (sym << 8)));
+        *(lane < 18 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)rv;
         __builtin_amdgcn_wave_barrier();
     }
 
     __device__ void pc_drop(uint32_t e)
     {
         pc_forget(e, 0, scr16(), 0);
-        *(lane < kSlotDepth ? &T.pc_pos[e * kSlotDepth + lane] : scr16()) = (uint16_t)0xFFFF;
-        *(lane == 0 ? &T.pc_meta[e] : scr32()) = 0u;
+        *(lane < 18 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)(lane < kSlotDepth ? 0xFFFFu : 0u);
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -194,7 +193,7 @@ struct Fgk {
     // levels 2(k&7), 2(k&7)+1 of entry k>>3; byte e of the ballot flags entry e.
     __device__ __forceinline__ void pc_swapped(uint32_t s, uint32_t l)
     {
-        const uint32_t q = reinterpret_cast<const uint32_t *>(T.pc_pos)[lane];
+        const uint32_t q = reinterpret_cast<const uint32_t *>(T.pc)[(lane >> 3) * (kRow / 2) + (lane & 7)];
         const uint32_t a = q ^ (s | (s << 16)), c = q ^ (l | (l << 16));
         const uint32_t z = ((a & 0xFFFFu) == 0) | ((a >> 16) == 0) | ((c & 0xFFFFu) == 0) | ((c >> 16) == 0);
         uint64_t m = ballot(z);
@@ -305,7 +304,7 @@ struct Fgk {
     {
         uint32_t k = 0;
         uint32_t s = vreg(s0);  // per-level work on the VALU (see vreg)
-        pv = kRoot + 1;
+        pv = kRoot;
         for (;;) {
             pv = lane == k ? s : pv;
             ++k;
@@ -348,37 +347,28 @@ struct Fgk {
             if (s >= kRoot) break;
         }
         bad |= s ^ kRoot;
-        rootw += kInc;
-        *(lane == 0 ? &T.wt[kRoot] : scr32()) = rootw;
+        const uint32_t r = uni(T.wt[kRoot]) + kInc;
+        *(lane == 0 ? &T.wt[kRoot] : scr32()) = r;
         __builtin_amdgcn_wave_barrier();
     }
 
-    // The same update when the path is already known: lanes lo..hi hold the positions of
-    // levels 0..hi-lo. Until the first swap the tree does not change, so every level's leader
-    // test reads the pre-update weights in parallel: a node leads its block when the next
-    // position is heavier, or when that position is its parent and the one after is heavier.
-    // Levels below the first one that fails increment with one store; the serial walk takes
-    // over from there (it also bumps the root).
-    __device__ __forceinline__ void update_path(uint32_t pv, uint32_t lo, uint32_t hi)
+    // The same update when the path is already known: lanes 0..d-1 hold the positions of
+    // levels 0..d-1, the other lanes kRoot. Until the first swap the tree does not change, so
+    // every level's leader test reads the pre-update words in parallel: a node leads its block
+    // when the next position is heavier, or when that position is its parent and the one after
+    // is heavier. The root lanes always lead (the sentinel above is heavier). Levels below the
+    // first one that fails increment with one store; without a failure the root lanes bump the
+    // root in the same store, otherwise the serial walk takes over (and bumps it at the end).
+    __device__ __forceinline__ void update_path(uint32_t a)
     {
-        const bool act = lane >= lo && lane <= hi;
-        const uint32_t a = act ? pv : kRoot + 1;
         const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1], w2 = T.wt[a + 2];
-        const uint32_t par = kWide ? T.up[a] : (w0 & 1023u);
-        const uint32_t lim = kWide ? w0 : (w0 | 1023u);
-        // no short-circuit: every term is computed, nothing branches per lane
-        const uint32_t ok = (uint32_t)(w1 > lim) | ((uint32_t)(a + 1 == par) & (uint32_t)(w2 > lim));
-        const uint64_t fail = ballot(act & !ok);
-        const uint32_t k = fail ? (uint32_t)__builtin_ctzll(fail) : hi + 1;
-        *(lane >= lo && lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
+        const uint32_t par = kWide ? (uint32_t)T.up[a] : (w0 & 1023u);
+        const uint32_t nxt = a + 1 == par ? w2 : w1;
+        const uint64_t fail = ballot(nxt <= (kWide ? w0 : (w0 | 1023u)));
+        const uint32_t k = fail ? (uint32_t)__builtin_ctzll(fail) : 64u;
+        *(lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
         __builtin_amdgcn_wave_barrier();
-        if (k <= hi) {
-            walk(lane_read(pv, k));
-        } else {
-            rootw += kInc;
-            *(lane == 0 ? &T.wt[kRoot] : scr32()) = rootw;
-            __builtin_amdgcn_wave_barrier();
-        }
+        if (fail) walk(lane_read(a, k));
     }
 };
 
@@ -577,25 +567,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
 
     // transform.cpp:363-384: per symbol encode (path before update), then update. Positions
     // stay in range by construction, so `bad` (a bug detector) is checked once per chunk.
-    auto code = [&](uint32_t sym) {
-        const uint32_t ws = uni(fgk.T.where[sym]);
+    const uint8_t *const sb = reinterpret_cast<const uint8_t *>(fgk.T.syms);
+    auto code = [&](uint32_t t) {  // symbol t of the LDS buffer
+        const uint32_t sv = vreg(sb[t]);
+        const uint32_t ws = uni(fgk.T.where[sv]);
         uint32_t s = ws & 1023u;
         if (ws >> 10) {  // path cached (never for a fresh symbol)
             uint32_t pv, bits;
             const uint32_t d = fgk.pc_get((ws >> 10) - 1, pv, bits);
-            fgk.update_path(pv, 0, d - 1);
+            fgk.update_path(pv);
             sink.put(bits, d);
             return;
         }
+        const uint32_t sym = uni(sv);
         const uint32_t fresh = s == 0;
         if (fresh) s = uni(fgk.split(sym));
         uint32_t pv;
         const uint32_t d = fgk.chase(s, pv);
         // bit k = code bit (position parity, left = even) of level k; read MSB first it is the
-        // root-to-leaf code
-        const uint64_t bits = ballot((pv & 1u) && lane < d);
+        // root-to-leaf code (the kRoot lanes are even)
+        const uint64_t bits = ballot(pv & 1u);
         fgk.pc_insert(sym, s, pv, d, (uint32_t)bits);
-        fgk.update_path(pv, 0, d - 1);
+        fgk.update_path(pv);
         if (fresh) {
             // the path starts at the new leaf, one level below the NYT whose code is sent
             // (huffman.cpp:44-50): drop that lowest bit, then 8 raw bits
@@ -614,23 +607,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         next = buf_load(rin, base + 256 + lane * 4);  // out of range past the end: reads 0
         const uint32_t m = min(256u, n32 - base);
         if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
-            uint32_t word = 0;
-            for (uint32_t j = 0; j < m; ++j) {
-                if ((j & 3u) == 0) word = lane_read(chunk, j >> 2);
-                code((word >> (8 * (j & 3u))) & 255u);
-            }
+            fgk.T.syms[lane] = chunk;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t t = 0; t < m; ++t) code(t);
             nsym += m;
             continue;
         }
         // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
         const uint32_t ns = rle_chunk<kSrc>(chunk, m, base + m == n32 ? 1u : 0u, cy, fgk.T.syms,
                                             fgk.scr32(), lane);
-        const uint32_t lo = fgk.T.syms[lane], hi = fgk.T.syms[64 + lane];
-        uint32_t word = 0;
-        for (uint32_t t = 0; t < ns; ++t) {
-            if ((t & 3u) == 0) word = lane_read(t < 256 ? lo : hi, (t >> 2) & 63u);
-            code((word >> (8 * (t & 3u))) & 255u);
-        }
+        for (uint32_t t = 0; t < ns; ++t) code(t);
         nsym += ns;
     }
 
@@ -795,36 +781,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
         const uint32_t i1 = min(n, i0 + 256);
         for (uint32_t i = i0; i < i1; ++i) {
             // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
-            // where the walk from the root stops, lane 64-j reads level j's position for the
-            // same prefix, so lanes lo..63 hold the path bottom-up. Codes longer than the
-            // tables reach go on from there bit by bit over a window of >= 33 bits.
+            // where the walk from the root stops (depth d <= 8); lane k < d reads level d-k's
+            // entry for the same prefix, the position of path level k (0 = the leaf). Codes
+            // longer than the tables reach go on bit by bit over a window of >= 33 bits.
             if (fgk.dirty | (uint32_t)(fgk.shortc >= kRefresh)) fgk.build_levels();
             if (in.nwin <= 32) in.refill();
             const uint32_t v = (uint32_t)(in.win >> 56);
             const uint32_t e8 = uni(fgk.T.lvl[254 + v]);
             uint32_t x = e8 & 1023u, depth = e8 >> 10;
-            const uint32_t jl = 64 - lane, jc = jl > 8 ? 8 : jl;
-            uint32_t pv = fgk.T.lvl[(1u << jc) - 2 + (v >> (8 - jc))] & 1023u;
-            pv = jl <= depth ? pv : kRoot + 1;
             uint32_t b = uni(fgk.T.body[x]);
-            if (b & kInner) {
+            uint32_t pv;
+            if (!(b & kInner)) {
+                const uint32_t j = lane < depth ? depth - lane : 8u;
+                pv = fgk.T.lvl[(1u << j) - 2 + (v >> (8 - j))] & 1023u;
+                pv = lane < depth ? pv : kRoot;
+                in.win <<= depth;
+                in.nwin -= depth;
+            } else {  // top-down first (depth j at lane 64-j), then turned bottom-up
                 fgk.shortc += depth < 8 ? 1u : 0u;
+                const uint32_t jl = 64 - lane, jc = jl > 8 ? 8 : jl;
+                uint32_t pt = fgk.T.lvl[(1u << jc) - 2 + (v >> (8 - jc))] & 1023u;
                 uint64_t w = in.win << depth;
                 do {
                     x = min((b & 255u) * 2 + (uint32_t)(w >> 63), x - 1);  // children sit below
                     w <<= 1;
-                    pv = lane == 63 - depth ? x : pv;
+                    pt = lane == 63 - depth ? x : pt;
                     ++depth;
                     b = uni(fgk.T.body[x]);
                 } while (b & kInner);
                 if (depth > in.nwin) {  // a code longer than the window (deep trees only)
                     x = kRoot;
                     depth = 0;
-                    pv = kRoot + 1;
                     b = uni(fgk.T.body[kRoot]);
                     while (b & kInner) {
                         x = min((b & 255u) * 2 + in.bit(), x - 1);
-                        pv = lane == 63 - depth ? x : pv;
+                        pt = lane == 63 - depth ? x : pt;
                         ++depth;
                         b = uni(fgk.T.body[x]);
                     }
@@ -833,20 +824,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                     in.nwin -= depth;
                 }
                 if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
-            } else {
-                in.win <<= depth;
-                in.nwin -= depth;
+                pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
+                pv = lane < depth ? pv : kRoot;
             }
             uint32_t sym;
-            if (b & kNyt) {
+            if (b & kNyt) {  // the new leaf below the NYT becomes level 0
                 sym = in.bits8();
                 x = uni(fgk.split(sym));
-                pv = lane == 63 - depth ? x : pv;
-                ++depth;
+                pv = __shfl_up(pv, 1, 64);
+                pv = lane == 0 ? x : pv;
             } else {
                 sym = b & 255u;
             }
-            fgk.update_path(pv, 64 - depth, 63);
+            fgk.update_path(pv);
 
             if (kDst == DST_SYMBOLS) {
                 out.byte(sym);

@@ -19,9 +19,15 @@ run() {  # run <name> <seconds> <rocprof args...>
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
 BENCH_ARGS=("$@")
-run stats 600 --kernel-trace --stats
-run pmc_inst 600 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE
-run pmc_wait 600 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_LDS_BANK_CONFLICT
-run pmc_fetch 600 --kernel-trace --pmc FETCH_SIZE
-run pmc_write 600 --kernel-trace --pmc WRITE_SIZE
+PASSES=${PASSES:-stats inst wait fetch write}  # subset: PASSES="inst wait" bash scripts/profile.sh ...
+for p in $PASSES; do
+    case $p in
+    stats) run stats 600 --kernel-trace --stats ;;
+    inst) run pmc_inst 600 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE ;;
+    wait) run pmc_wait 600 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_LDS_BANK_CONFLICT ;;
+    branch) run pmc_branch 600 --kernel-trace --pmc SQ_INSTS_BRANCH SQ_INSTS_SENDMSG SQ_INSTS_VMEM SQ_INSTS_FLAT GRBM_GUI_ACTIVE ;;
+    fetch) run pmc_fetch 600 --kernel-trace --pmc FETCH_SIZE ;;
+    write) run pmc_write 600 --kernel-trace --pmc WRITE_SIZE ;;
+    esac
+done
 echo done
