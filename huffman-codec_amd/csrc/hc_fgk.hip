@@ -55,7 +55,7 @@ struct alignas(16) Tree {
     uint16_t body[516];
     uint16_t where[kDec ? 2 : 256];   // encoder: symbol -> position | (entry + 1) << 10; 0 = unseen
     uint16_t up[kWide ? 516 : 2];     // wide: parent position
-    alignas(8) uint32_t syms[kDec ? 1 : 128];  // encoder: MNP-5 symbols of one 256-byte chunk
+    alignas(8) uint32_t syms[kDec ? 64 : 128];  // MNP-5 symbols: encoder one chunk, decoder one block
     // encoder path cache, entry e = row e: positions of levels 0..15 (kRoot above the path),
     // [16] code bits, [17] depth | valid << 5 | symbol << 8, [18..19] unused. One lane-based
     // address reads a lane's position and (lane 0) the row's metadata.
@@ -673,36 +673,88 @@ struct BitSource {
     }
 };
 
-// VGPR byte stage for decoded output: 256 bytes per coalesced buffer store. pos may run past
-// the capacity (then bytes are only counted, the range check drops the stores).
-struct ByteSink {
-    rsrc_t rs;
-    uint32_t lane;
-    uint32_t pos;  // bytes produced
-    uint32_t cur;  // partial word
-    uint32_t stage;
+// ------------------------------------------------------- RLE + diff revert (decoder) ------
 
-    __device__ __forceinline__ void byte(uint32_t b)
-    {
-        cur |= b << (8 * (pos & 3u));
-        ++pos;
-        if ((pos & 3u) == 0) {
-            stage = lane == ((pos >> 2) - 1) % 64u ? cur : stage;
-            cur = 0;
-            if ((pos & 255u) == 0) buf_store(rs, pos - 256 + lane * 4, stage);
+// transform.cpp:137-159 (RLE revert) then 231-239 (diff revert) for one block of <= 256
+// symbols, all lanes at once (model and derivation: tests/revert_block_model.py). The serial
+// revert is a 4-state machine on the run counter r: in state 3 a symbol is a count (it emits
+// that many copies of the previous symbol, r -> 0), else a literal (r -> r+1 when it repeats the
+// previous symbol and r is 1 or 2, otherwise r -> 1). A symbol's transition is one of two
+// functions on {0..3} (4 x 2 bits); a wave scan of their compositions gives each symbol's
+// state, scans of output lengths and diff sums give each lane's output offset and running byte.
+struct RevCarry {
+    uint32_t r;     // machine state after the last symbol
+    uint32_t last;  // last symbol
+    uint32_t prev;  // last output byte (diff model)
+};
+
+constexpr uint32_t kFeq = 1u | 2u << 2 | 3u << 4;  // r: 0->1 1->2 2->3 3->0
+constexpr uint32_t kFne = 1u | 1u << 2 | 1u << 4;  // r: 0->1 1->1 2->1 3->0
+constexpr uint32_t kFid = 0u | 1u << 2 | 2u << 4 | 3u << 6;
+
+__device__ __forceinline__ uint32_t fsm_compose(uint32_t g, uint32_t f)  // x -> g(f(x))
+{
+    uint32_t h = 0;
+    for (uint32_t x = 0; x < 4; ++x) {
+        const uint32_t y = (f >> (2 * x)) & 3u;
+        h |= ((g >> (2 * y)) & 3u) << (2 * x);
+    }
+    return h;
+}
+
+// lane l holds symbols 4l..4l+3 (m valid); bytes go to the stream's output at pos onwards (the
+// buffer range check drops what is past the capacity); returns the bytes produced
+__device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCarry &cy, uint32_t dmask,
+                                                 rsrc_t rs, uint32_t pos, uint32_t lane)
+{
+    const uint32_t up = __shfl_up(x4, 1, 64);
+    const uint32_t xp = (x4 << 8) | ((lane == 0 ? (cy.last << 24) : up) >> 24);  // previous symbols
+    const uint32_t i0 = lane * 4;
+    uint32_t f[4], F = kFid;
+    for (uint32_t b = 0; b < 4; ++b) {
+        f[b] = i0 + b < m ? (byte_of(x4, b) == byte_of(xp, b) ? kFeq : kFne) : kFid;
+        F = fsm_compose(f[b], F);
+    }
+    uint32_t inc = F;  // inclusive scan: lanes 0..l applied in order
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t g = __shfl_up(inc, off, 64);
+        inc = lane >= off ? fsm_compose(inc, g) : inc;
+    }
+    const uint32_t ex = __shfl_up(inc, 1, 64);
+    uint32_t r = ((lane == 0 ? kFid : ex) >> (2 * cy.r)) & 3u;
+    uint32_t len[4], c[4], tot = 0, ds = 0;
+    for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t sb = byte_of(x4, b), pb = byte_of(xp, b);
+        const bool valid = i0 + b < m;
+        const bool cnt = r == 3;
+        len[b] = valid ? (cnt ? sb : 1u) : 0u;
+        c[b] = cnt ? pb : sb;
+        ds += valid ? (cnt ? sb * pb : sb) : 0u;
+        tot += len[b];
+        r = (f[b] >> (2 * r)) & 3u;
+    }
+    // exclusive scans of (length, diff sum mod 256), packed: both halves stay below 2^16
+    const uint32_t mine = tot | ((ds & 255u) << 16);
+    uint32_t acc = mine;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t g = __shfl_up(acc, off, 64);
+        acc += lane >= off ? g : 0u;
+    }
+    const uint32_t exc = acc - mine;
+    uint32_t prev = (cy.prev + (exc >> 16)) & 255u;
+    uint32_t o = pos + (exc & 0xFFFFu);
+    for (uint32_t b = 0; b < 4; ++b) {
+        for (uint32_t k = 0; k < len[b]; ++k) {
+            prev = ((prev & dmask) + c[b]) & 255u;
+            buf_store8(rs, o++, prev);
         }
     }
-    __device__ __forceinline__ void finish()
-    {
-        const uint32_t wbase = (pos >> 2) & ~63u;
-        const uint32_t full = (pos >> 2) & 63u;
-        const uint32_t tail = pos & 3u;
-        const uint32_t off = (wbase + lane) * 4;
-        buf_store(rs, lane < full ? off : kDrop, stage);
-        for (uint32_t b = 0; b < 3; ++b)
-            buf_store8(rs, lane == full && b < tail ? off + b : kDrop, cur >> (8 * b));
-    }
-};
+    const uint32_t all = lane_read(acc, 63);
+    cy.r = (lane_read(inc, 63) >> (2 * cy.r)) & 3u;
+    cy.last = byte_of(lane_read(x4, (m - 1) >> 2), (m - 1) & 3u);
+    cy.prev = (cy.prev + (all >> 16)) & 255u;
+    return all & 0xFFFFu;
+}
 
 template <bool kWide, int kDst>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void decode_kernel(Batch bt)
@@ -757,15 +809,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     in.win <<= 8;
     in.nwin -= 8;
 
-    ByteSink out;
-    out.rs = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
-    out.lane = lane;
-    out.pos = 0;
-    out.cur = 0;
-    out.stage = 0;
-
+    const rsrc_t rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
+    uint32_t pos = 0;  // output bytes produced
     const uint32_t dmask = kDst == DST_RAW && (flags & 0x80u) ? 255u : 0u;  // diff model
-    uint32_t prev = 0, run_byte = 0, run = 0;
+    RevCarry rc = {0, 0, 0};
+    uint8_t *const sbuf = reinterpret_cast<uint8_t *>(fgk.T.syms);  // this block's symbols
     const uint32_t n = (uint32_t)count;
     // bits read from the stream = words pushed into the window * 32 - bits still in it; the
     // payload starts at bit 72. A stream that ends early decodes zero bits past its end (the
@@ -777,7 +825,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     };
 
     for (uint32_t i0 = 0; i0 < n; i0 += 256) {
-        if (fgk.bad || out.pos > kMaxBufBytes || consumed() > payload_bits + 64) break;
+        if (fgk.bad || pos > kMaxBufBytes || consumed() > payload_bits + 64) break;
         const uint32_t i1 = min(n, i0 + 256);
         for (uint32_t i = i0; i < i1; ++i) {
             // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
@@ -838,33 +886,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             }
             fgk.update_path(pv);
 
-            if (kDst == DST_SYMBOLS) {
-                out.byte(sym);
-                continue;
-            }
-            // transform.cpp:137-159 (RLE revert), then transform.cpp:231-239 (diff revert)
-            if (run == 3) {
-                for (uint32_t r = 0; r < sym; ++r) {
-                    prev = ((prev & dmask) + run_byte) & 255u;
-                    out.byte(prev);
-                }
-                run = 0;
-            } else {
-                prev = ((prev & dmask) + sym) & 255u;
-                out.byte(prev);
-                run = sym == run_byte ? run + 1 : 1;
-                run_byte = sym;
-            }
+            sbuf[i - i0] = (uint8_t)sym;  // every lane stores the same byte
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t x4 = fgk.T.syms[lane];
+        const uint32_t m = i1 - i0;
+        if (kDst == DST_SYMBOLS) {
+            for (uint32_t b = 0; b < 4; ++b)
+                buf_store8(rout, lane * 4 + b < m ? pos + lane * 4 + b : kDrop, byte_of(x4, b));
+            pos += m;
+        } else {
+            pos += revert_block(x4, m, rc, dmask, rout, pos, lane);
         }
     }
     if (consumed() > payload_bits) st = HC_ERR_HUFFMAN;  // ran past the payload
-    else if (out.pos > kMaxBufBytes) st = HC_ERR_UNSUPPORTED;  // beyond the device path's offsets
+    else if (pos > kMaxBufBytes) st = HC_ERR_UNSUPPORTED;  // beyond the device path's offsets
     if (fgk.bad) st = HC_ERR_DEVICE;
-    if (st == 0) out.finish();
-    if (st == 0 && out.pos > cap) st = HC_ERR_CAPACITY;
+    if (st == 0 && pos > cap) st = HC_ERR_CAPACITY;
     if (lane == 0) {
         bt.status[sid] = (int32_t)st;
-        bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? out.pos : 0;
+        bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? pos : 0;
     }
 }
 

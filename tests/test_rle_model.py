@@ -21,3 +21,30 @@ def test_chunked_rle_equals_serial(oracle_mod):
         raw = oracle_mod.synth(("photo", "grad", "noise")[k % 3], k, 64, 64).tobytes()
         for diff in (False, True):
             assert rle_chunked(raw, diff) == oracle_mod.rle(oracle_mod.diff(raw) if diff else raw)
+
+
+# ---- decoder side: lane-parallel RLE + diff revert (tests/revert_block_model.py)
+import random as _random
+
+import revert_block_model as _rb
+
+
+def test_revert_block_model_streams(oracle_mod):
+    for kind in ("photo", "grad", "noise"):
+        raw = oracle_mod.synth(kind, 2, 128, 96).tobytes()
+        for diff in (True, False):
+            sym = oracle_mod.rle(oracle_mod.diff(raw) if diff else raw)
+            assert _rb.revert_blocked(sym, diff) == raw, (kind, diff)
+
+
+def test_revert_block_model_random(oracle_mod):
+    rng = _random.Random(11)
+    for t in range(120):
+        n = rng.randrange(0, 1100)
+        alpha = rng.choice([2, 3, 5, 256])
+        sym = bytes(rng.randrange(alpha) for _ in range(n))
+        for diff in (True, False):
+            want = oracle_mod.unrle(sym)
+            if diff:
+                want = oracle_mod.undiff(want)
+            assert _rb.revert_blocked(sym, diff) == want, (t, diff)
