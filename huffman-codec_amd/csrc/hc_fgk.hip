@@ -36,9 +36,12 @@ constexpr int kWaves = 4;
 constexpr uint32_t kMaxBufBytes = 0x7FFFFF00u;  // per-stream limit of the 32-bit buffer offsets
 constexpr uint32_t kDrop = 0x7FFFFFF8u;         // buffer offset past every range: access dropped
 
-constexpr uint32_t kSlots = 8;      // encoder path cache: entries
-constexpr uint32_t kSlotDepth = 16; // deepest cached path (its code bits fit 16 bits)
-constexpr uint32_t kRow = 20;       // u16 per cache entry
+constexpr uint32_t kSlots = 16;     // encoder path cache: entries
+constexpr uint32_t kSlotDepth = 12; // deepest cached path
+constexpr uint32_t kRow = 16;       // u16 per cache entry
+constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte chunk, <= 342
+                                    // (a byte emits 2 only at a run start that follows a run of
+                                    // >= 3, so such bytes are >= 3 apart)
 constexpr uint32_t kRefresh = 16;   // decoder: rebuild the level tables after this many lookups
                                     // they left short of depth 8
 constexpr uint32_t kMarkShift = 10; // decoder: body bits 10..15 = table generation (per position)
@@ -55,11 +58,11 @@ struct alignas(16) Tree {
     uint16_t body[516];
     uint16_t where[kDec ? 2 : 256];   // encoder: symbol -> position | (entry + 1) << 10; 0 = unseen
     uint16_t up[kWide ? 516 : 2];     // wide: parent position
-    alignas(8) uint32_t syms[kDec ? 64 : 128];  // MNP-5 symbols: encoder one chunk, decoder one block
-    // encoder path cache, entry e = row e: positions of levels 0..15 (kRoot above the path),
-    // [16] code bits, [17] depth | valid << 5 | symbol << 8, [18..19] unused. One lane-based
+    // encoder path cache, entry e = row e: positions of levels 0..11 (kRoot above the path),
+    // [12] code bits, [13] depth | valid << 5 | symbol << 8, [14..15] unused. One lane-based
     // address reads a lane's position and (lane 0) the row's metadata.
-    alignas(8) uint16_t pc[kDec ? 2 : kSlots * kRow];
+    alignas(16) uint16_t pc[kDec ? 2 : kSlots * kRow];
+    alignas(8) uint32_t syms[kDec ? 64 : kSymWords];  // MNP-5 symbols: encoder one chunk, decoder one block
     // decoder level tables: level j (1..8) at 2^j - 2 + prefix: position | depth << 10 where
     // the walk from the root along the prefix's bits stops
     uint16_t lvl[kDec ? 512 : 2];
@@ -118,13 +121,14 @@ struct Fgk {
     uint32_t lane;
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
-    uint32_t pc_next;  // encoder: next cache entry to fill (round robin)
+    uint32_t pc_next;  // encoder: clock hand of the path cache
+    uint32_t pc_ref;   // encoder: reference bits of the entries
     uint32_t gen;      // decoder: generation of the level tables
     uint32_t dirty;    // decoder: a swap moved a position the tables walk through
     uint32_t shortc;   // decoder: lookups the tables left short since the last build
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
-        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), gen(0), dirty(1), shortc(0)
+        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_ref(0), gen(0), dirty(1), shortc(0)
     {
         // huffman.cpp:23-31: a lone NYT root
         for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
@@ -151,56 +155,75 @@ struct Fgk {
     // A path changes only when a swap moves a position on it; splits touch no symbol's path.
 
     // hit: entry e's path to lanes 0..d-1 (kRoot above), its code bits; returns d
-    __device__ __forceinline__ uint32_t pc_get(uint32_t e, uint32_t &pv, uint32_t &bits) const
+    __device__ __forceinline__ uint32_t pc_get(uint32_t e, uint32_t &pv, uint32_t &bits)
     {
-        const uint16_t *row = &T.pc[e * kRow] + (lane & (kSlotDepth - 1));  // lane 0: row start
+        const uint16_t *row = &T.pc[e * kRow] + (lane & 15u);  // lane 0: the row's start
         pv = lane < kSlotDepth ? (uint32_t)row[0] : kRoot;
-        bits = uni(row[16]);
-        return uni(row[17]) & 31u;
+        bits = uni(row[kSlotDepth]);
+        pc_ref |= 1u << e;
+        return uni(row[kSlotDepth + 1]) & 31u;
     }
 
     // forget entry e (its symbol's where[] keeps only the position: level 0 of the path)
-    __device__ __forceinline__ void pc_forget(uint32_t e, uint32_t lane0, uint16_t *other, uint32_t oval)
+    __device__ __forceinline__ void pc_forget(uint32_t e, uint16_t *other, uint32_t oval)
     {
-        const uint32_t m = uni(T.pc[e * kRow + 17]);
+        const uint32_t m = uni(T.pc[e * kRow + kSlotDepth + 1]);
         const uint32_t opos = uni(T.pc[e * kRow]);
-        uint16_t *q = lane == lane0 ? ((m >> 5) & 1u ? &T.where[m >> 8] : scr16()) : other;
-        *q = (uint16_t)(lane == lane0 ? opos : oval);
+        uint16_t *q = lane == 0 ? ((m >> 5) & 1u ? &T.where[m >> 8] : scr16()) : other;
+        *q = (uint16_t)(lane == 0 ? opos : oval);
     }
 
-    // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot)
+    // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot). The
+    // clock hand skips (and clears) referenced entries.
     __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t bits)
     {
         if (d > kSlotDepth) return;
-        const uint32_t e = pc_next;
+        const uint32_t h = pc_next;
+        const uint32_t rot = ((pc_ref >> h) | (pc_ref << (kSlots - h))) & 0xFFFFu;
+        const uint32_t k = rot == 0xFFFFu ? 0u : (uint32_t)__builtin_ctz(~rot);
+        const uint32_t passed = rot == 0xFFFFu ? 0xFFFFu : ((1u << k) - 1u);
+        const uint32_t e = (h + k) & (kSlots - 1);
+        pc_ref &= ~(((passed << h) | (passed >> (kSlots - h))) & 0xFFFFu);
+        pc_ref |= 1u << e;
         pc_next = (e + 1) & (kSlots - 1);
         // lane 0: the evicted symbol forgets its entry; lane 1: this symbol takes it
-        pc_forget(e, 0, lane == 1 ? &T.where[sym] : scr16(), s | ((e + 1) << 10));
-        // lanes 0..15 the positions, 16 the code bits, 17 depth | valid | symbol
-        const uint32_t rv = lane < kSlotDepth ? pv : (lane == 16 ? bits : (d | 32u | (sym << 8)));
-        *(lane < 18 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)rv;
+        pc_forget(e, lane == 1 ? &T.where[sym] : scr16(), s | ((e + 1) << 10));
+        // lanes 0..11 the positions, 12 the code bits, 13 depth | valid | symbol
+        const uint32_t rv = lane < kSlotDepth ? pv : (lane == kSlotDepth ? bits : (d | 32u | (sym << 8)));
+        *(lane < kSlotDepth + 2 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)rv;
         __builtin_amdgcn_wave_barrier();
     }
 
     __device__ void pc_drop(uint32_t e)
     {
-        pc_forget(e, 0, scr16(), 0);
-        *(lane < 18 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)(lane < kSlotDepth ? 0xFFFFu : 0u);
+        pc_forget(e, scr16(), 0);
+        *(lane < kSlotDepth + 2 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)(lane < kSlotDepth ? 0xFFFFu : 0u);
         __builtin_amdgcn_wave_barrier();
+        pc_ref &= ~(1u << e);
     }
 
-    // positions s and l traded contents: drop every cached path through either. Lane k reads
-    // levels 2(k&7), 2(k&7)+1 of entry k>>3; byte e of the ballot flags entry e.
+    // positions s and l traded contents: drop every cached path through either. Per read,
+    // lane k holds levels 2(k&7), 2(k&7)+1 of entry k>>3 (+8 in the second read); words 6..7 of
+    // a row are metadata. Byte e of a ballot flags an entry.
     __device__ __forceinline__ void pc_swapped(uint32_t s, uint32_t l)
     {
-        const uint32_t q = reinterpret_cast<const uint32_t *>(T.pc)[(lane >> 3) * (kRow / 2) + (lane & 7)];
-        const uint32_t a = q ^ (s | (s << 16)), c = q ^ (l | (l << 16));
-        const uint32_t z = ((a & 0xFFFFu) == 0) | ((a >> 16) == 0) | ((c & 0xFFFFu) == 0) | ((c >> 16) == 0);
-        uint64_t m = ballot(z);
-        while (m) {
-            const uint32_t e = (uint32_t)__builtin_ctzll(m) >> 3;
-            m &= ~(0xFFull << (8 * e));
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(T.pc);
+        const uint32_t ss = s | (s << 16), ll = l | (l << 16);
+        auto hit = [&](uint32_t q) -> uint32_t {
+            const uint32_t a = q ^ ss, c = q ^ ll;
+            return (uint32_t)((lane & 7u) < kSlotDepth / 2) &
+                   (((a & 0xFFFFu) == 0) | ((a >> 16) == 0) | ((c & 0xFFFFu) == 0) | ((c >> 16) == 0));
+        };
+        uint64_t m0 = ballot(hit(w[lane])), m1 = ballot(hit(w[64 + lane]));
+        while (m0) {
+            const uint32_t e = (uint32_t)__builtin_ctzll(m0) >> 3;
+            m0 &= ~(0xFFull << (8 * e));
             pc_drop(e);
+        }
+        while (m1) {
+            const uint32_t e = (uint32_t)__builtin_ctzll(m1) >> 3;
+            m1 &= ~(0xFFull << (8 * e));
+            pc_drop(e + 8);
         }
     }
 

@@ -4,8 +4,8 @@ The slot-form tree (oracle/hc_oracle.c: sl_*) changes shape 
 (new leaves below the NYT position) and at a swap (the contents of positions s and lead trade
 places, huffman.cpp:186-217). Two caches exploit that:
 
-* path cache (encoder and decoder): the root paths (positions, code bits) of the last 8 coded
-  symbols, round robin. A swap of s and lead stales exactly the cached paths that contain s or
+* path cache (encoder): the root paths (positions, code bits) of up to 16 recently coded
+  symbols whose paths are at most 12 deep, clock replacement. A swap of s and lead stales exactly the cached paths that contain s or
   lead; a split stales none (the NYT position is on no symbol's path).
 * level tables (decoder): for j = 1..8 and each j-bit prefix, the position reached from the root
   by reading the prefix's bits (stopping at a leaf). The 8-bit table finds the leaf; lane 64-j
@@ -21,8 +21,8 @@ a fresh chase and that a table lookup equals a full descent, and returns hit / r
 ROOT = 512
 INNER = 0x100
 NYT = 0x200
-SLOTS = 8
-MAXD = 16  # deepest cached path
+SLOTS = 16
+MAXD = 12  # deepest cached path
 REFRESH = 16  # rebuild the level tables after this many lookups they left short
 
 
@@ -88,9 +88,14 @@ class Tree:
 
 
 class PathCache:
+    """Clock replacement (second chance), as the kernel: a hit sets the entry's reference
+    bit; an insert takes the first entry from `next` on whose bit is clear, clearing the bits
+    it passes (all of them when every bit is set); dropping an entry clears its bit."""
+
     def __init__(self):
         self.ent = [None] * SLOTS  # (sym, pv)
         self.slot = {}             # sym -> slot
+        self.ref = 0               # reference bits
         self.next = 0
         self.hits = self.misses = self.inval = 0
 
@@ -100,13 +105,22 @@ class PathCache:
             self.misses += 1
             return None
         self.hits += 1
+        self.ref |= 1 << e
         return self.ent[e][1]
 
     def insert(self, sym, pv):
         if len(pv) > MAXD:
             return
-        e = self.next
-        self.next = (self.next + 1) % SLOTS
+        k = 0
+        while k < SLOTS and self.ref >> ((self.next + k) % SLOTS) & 1:
+            k += 1
+        if k == SLOTS:
+            self.ref, k = 0, 0
+        for j in range(k):
+            self.ref &= ~(1 << ((self.next + j) % SLOTS))
+        e = (self.next + k) % SLOTS
+        self.next = (e + 1) % SLOTS
+        self.ref |= 1 << e
         if self.ent[e] is not None:
             self.slot.pop(self.ent[e][0], None)
         self.ent[e] = (sym, list(pv))
@@ -117,6 +131,7 @@ class PathCache:
             if self.ent[e] is not None and (s in self.ent[e][1] or lead in self.ent[e][1]):
                 self.slot.pop(self.ent[e][0], None)
                 self.ent[e] = None
+                self.ref &= ~(1 << e)
                 self.inval += 1
 
 
