@@ -124,11 +124,11 @@ struct Fgk {
     uint32_t pc_next;  // encoder: clock hand of the path cache
     uint32_t pc_ref;   // encoder: reference bits of the entries
     uint32_t gen;      // decoder: generation of the level tables
-    uint32_t dirty;    // decoder: a swap moved a position the tables walk through
-    uint32_t shortc;   // decoder: lookups the tables left short since the last build
+    uint32_t stale;    // decoder: >= kRefresh = rebuild the level tables (a swap moved a position
+                       // they walk through: += kRefresh; a lookup they left short: += 1)
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
-        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_ref(0), gen(0), dirty(1), shortc(0)
+        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_ref(0), gen(0), stale(kRefresh)
     {
         // huffman.cpp:23-31: a lone NYT root
         for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
@@ -250,8 +250,7 @@ struct Fgk {
             }
             __builtin_amdgcn_wave_barrier();
         }
-        dirty = 0;
-        shortc = 0;
+        stale = 0;
     }
 
     // huffman.cpp:99-111: split NYT at t -> NYT at t-2 (left), symbol leaf at t-1 (right).
@@ -286,7 +285,7 @@ struct Fgk {
         if (kDec) {  // generation marks stay with the positions
             const uint32_t keep = ((lane & 1) ? bl : bs) & ~0x3FFu;
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & 0x3FFu) | keep);
-            dirty |= (uint32_t)((bs >> kMarkShift) == gen) | (uint32_t)((bl >> kMarkShift) == gen);
+            stale += (((bs >> kMarkShift) == gen) | ((bl >> kMarkShift) == gen)) ? kRefresh : 0u;
         } else {
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
             *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
@@ -661,7 +660,7 @@ struct BitSource {
     rsrc_t rs;
     uint32_t lane;
     uint32_t cbase;  // byte offset of chunk lane 0
-    uint32_t chunk;
+    uint32_t chunk;  // big-endian words (byte-swapped once per load, on the lanes)
     uint32_t ridx;
     uint64_t win;  // upcoming bits, MSB-aligned
     uint32_t nwin; // valid bits in win
@@ -669,12 +668,12 @@ struct BitSource {
     // push the next 32 bits (needs nwin <= 32)
     __device__ __forceinline__ void refill()
     {
-        const uint32_t w = __builtin_bswap32(lane_read(chunk, ridx));
+        const uint32_t w = lane_read(chunk, ridx);
         win |= (uint64_t)w << (32 - nwin);
         nwin += 32;
         if (++ridx == 64) {
             cbase += 256;
-            chunk = buf_load(rs, cbase + lane * 4);
+            chunk = __builtin_bswap32(buf_load(rs, cbase + lane * 4));
             ridx = 0;
         }
     }
@@ -824,7 +823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     in.rs = rin;
     in.lane = lane;
     in.cbase = 0;
-    in.chunk = hdr;
+    in.chunk = __builtin_bswap32(hdr);
     in.ridx = 2;
     in.win = 0;
     in.nwin = 0;
@@ -855,7 +854,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // where the walk from the root stops (depth d <= 8); lane k < d reads level d-k's
             // entry for the same prefix, the position of path level k (0 = the leaf). Codes
             // longer than the tables reach go on bit by bit over a window of >= 33 bits.
-            if (fgk.dirty | (uint32_t)(fgk.shortc >= kRefresh)) fgk.build_levels();
+            if (fgk.stale >= kRefresh) fgk.build_levels();
             if (in.nwin <= 32) in.refill();
             const uint32_t v = (uint32_t)(in.win >> 56);
             const uint32_t e8 = uni(fgk.T.lvl[254 + v]);
@@ -863,13 +862,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             uint32_t b = uni(fgk.T.body[x]);
             uint32_t pv;
             if (!(b & kInner)) {
-                const uint32_t j = lane < depth ? depth - lane : 8u;
-                pv = fgk.T.lvl[(1u << j) - 2 + (v >> (8 - j))] & 1023u;
+                // level j's entry for prefix v >> (8 - j) sits at 2^j - 2 + (v >> (8 - j))
+                // = ((256 | v) >> (8 - j)) - 2; lane k needs j = depth - k (idle lanes: any)
+                const uint32_t sh = min(8 - depth + lane, 7u);
+                pv = fgk.T.lvl[((256u | v) >> sh) - 2] & 1023u;
                 pv = lane < depth ? pv : kRoot;
                 in.win <<= depth;
                 in.nwin -= depth;
             } else {  // top-down first (depth j at lane 64-j), then turned bottom-up
-                fgk.shortc += depth < 8 ? 1u : 0u;
+                fgk.stale += depth < 8 ? 1u : 0u;
                 const uint32_t jl = 64 - lane, jc = jl > 8 ? 8 : jl;
                 uint32_t pt = fgk.T.lvl[(1u << jc) - 2 + (v >> (8 - jc))] & 1023u;
                 uint64_t w = in.win << depth;
