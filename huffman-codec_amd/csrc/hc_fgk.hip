@@ -59,7 +59,8 @@ struct alignas(16) Tree {
     uint16_t where[kDec ? 2 : 256];   // encoder: symbol -> position | (entry + 1) << 10; 0 = unseen
     uint16_t up[kWide ? 516 : 2];     // wide: parent position
     // encoder path cache, entry e = row e: positions of levels 0..11 (kRoot above the path),
-    // [12] code bits, [13] depth | valid << 5 | symbol << 8, [14..15] unused. One lane-based
+    // [12] code record 1 << depth | code bits, [13] depth | valid << 5 | symbol << 8, [14..15]
+    // unused. One lane-based
     // address reads a lane's position and (lane 0) the row's metadata.
     alignas(16) uint16_t pc[kDec ? 2 : kSlots * kRow];
     alignas(8) uint32_t syms[kDec ? 64 : kSymWords];  // MNP-5 symbols: encoder one chunk, decoder one block
@@ -84,6 +85,14 @@ __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool any(bool p) { return ballot(p) != 0; }
+// lowest set bit of a wave mask, 0xFFFFFFFF for 0 (s_ff1_i32_b64 without the zero test)
+__device__ __forceinline__ uint32_t ff1(uint64_t m)
+{
+    uint32_t r;
+    asm volatile("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+    return r;
+}
 // A wave-uniform value held in a VGPR: hiding its uniformity from the compiler moves the
 // arithmetic on it from the (saturated) scalar unit to the vector ALUs. Branches on such
 // values go through ballot(), which is uniform again.
@@ -122,13 +131,16 @@ struct Fgk {
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
     uint32_t pc_next;  // encoder: clock hand of the path cache
-    uint32_t pc_ref;   // encoder: reference bits of the entries
+    uint32_t pc_ref;   // encoder: reference bits of the entries (bit e + 1 = entry e), kept in a
+                       // VGPR: a hit sets its bit on the VALU
     uint32_t gen;      // decoder: generation of the level tables
     uint32_t stale;    // decoder: >= kRefresh = rebuild the level tables (a swap moved a position
                        // they walk through: += kRefresh; a lookup they left short: += 1)
+    const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow] (entry e's row = e - 1)
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
-        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_ref(0), gen(0), stale(kRefresh)
+        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_ref(0), gen(0), stale(kRefresh),
+          pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
         for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
@@ -154,14 +166,14 @@ struct Fgk {
     // ---- encoder path cache: root paths of recently coded symbols (tests/fgk_cache_model.py).
     // A path changes only when a swap moves a position on it; splits touch no symbol's path.
 
-    // hit: entry e's path to lanes 0..d-1 (kRoot above), its code bits; returns d
-    __device__ __forceinline__ uint32_t pc_get(uint32_t e, uint32_t &pv, uint32_t &bits)
+    // hit: row of entry e (lane k < 12: position of level k, lanes >= d read kRoot padding);
+    // returns the row's code record (word 12, see RecSink) in an SGPR
+    __device__ __forceinline__ uint32_t pc_get(uint32_t e, uint32_t &pv)
     {
-        const uint16_t *row = &T.pc[e * kRow] + (lane & 15u);  // lane 0: the row's start
-        pv = lane < kSlotDepth ? (uint32_t)row[0] : kRoot;
-        bits = uni(row[kSlotDepth]);
-        pc_ref |= 1u << e;
-        return uni(row[kSlotDepth + 1]) & 31u;
+        const uint32_t pr = pc_lane[e * kRow];  // one lane-parallel read of the whole row
+        pv = lane < kSlotDepth ? pr : kRoot;
+        pc_ref = vreg(pc_ref | (1u << e));
+        return lane_read(pr, kSlotDepth);
     }
 
     // forget entry e (its symbol's where[] keeps only the position: level 0 of the path)
@@ -173,23 +185,26 @@ struct Fgk {
         *q = (uint16_t)(lane == 0 ? opos : oval);
     }
 
-    // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot). The
-    // clock hand skips (and clears) referenced entries.
-    __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t bits)
+    // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot) and
+    // its code record rec (1 << d | code bits). The clock hand skips (and clears) referenced
+    // entries.
+    __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t rec)
     {
         if (d > kSlotDepth) return;
         const uint32_t h = pc_next;
-        const uint32_t rot = ((pc_ref >> h) | (pc_ref << (kSlots - h))) & 0xFFFFu;
+        uint32_t ref = uni(pc_ref) >> 1;
+        const uint32_t rot = ((ref >> h) | (ref << (kSlots - h))) & 0xFFFFu;
         const uint32_t k = rot == 0xFFFFu ? 0u : (uint32_t)__builtin_ctz(~rot);
         const uint32_t passed = rot == 0xFFFFu ? 0xFFFFu : ((1u << k) - 1u);
         const uint32_t e = (h + k) & (kSlots - 1);
-        pc_ref &= ~(((passed << h) | (passed >> (kSlots - h))) & 0xFFFFu);
-        pc_ref |= 1u << e;
+        ref &= ~(((passed << h) | (passed >> (kSlots - h))) & 0xFFFFu);
+        ref |= 1u << e;
+        pc_ref = vreg(ref << 1);
         pc_next = (e + 1) & (kSlots - 1);
         // lane 0: the evicted symbol forgets its entry; lane 1: this symbol takes it
         pc_forget(e, lane == 1 ? &T.where[sym] : scr16(), s | ((e + 1) << 10));
-        // lanes 0..11 the positions, 12 the code bits, 13 depth | valid | symbol
-        const uint32_t rv = lane < kSlotDepth ? pv : (lane == kSlotDepth ? bits : (d | 32u | (sym << 8)));
+        // lanes 0..11 the positions, 12 the code record, 13 depth | valid | symbol
+        const uint32_t rv = lane < kSlotDepth ? pv : (lane == kSlotDepth ? rec : (d | 32u | (sym << 8)));
         *(lane < kSlotDepth + 2 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)rv;
         __builtin_amdgcn_wave_barrier();
     }
@@ -199,7 +214,7 @@ struct Fgk {
         pc_forget(e, scr16(), 0);
         *(lane < kSlotDepth + 2 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)(lane < kSlotDepth ? 0xFFFFu : 0u);
         __builtin_amdgcn_wave_barrier();
-        pc_ref &= ~(1u << e);
+        pc_ref = vreg(pc_ref & ~(2u << e));
     }
 
     // positions s and l traded contents: drop every cached path through either. Per read,
@@ -381,16 +396,21 @@ struct Fgk {
     // is heavier. The root lanes always lead (the sentinel above is heavier). Levels below the
     // first one that fails increment with one store; without a failure the root lanes bump the
     // root in the same store, otherwise the serial walk takes over (and bumps it at the end).
-    __device__ __forceinline__ void update_path(uint32_t a)
+    __device__ __forceinline__ uint32_t update_fast(uint32_t a)
     {
         const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1], w2 = T.wt[a + 2];
         const uint32_t par = kWide ? (uint32_t)T.up[a] : (w0 & 1023u);
         const uint32_t nxt = a + 1 == par ? w2 : w1;
         const uint64_t fail = ballot(nxt <= (kWide ? w0 : (w0 | 1023u)));
-        const uint32_t k = fail ? (uint32_t)__builtin_ctzll(fail) : 64u;
+        const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
         *(lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
         __builtin_amdgcn_wave_barrier();
-        if (fail) walk(lane_read(a, k));
+        return k;
+    }
+    __device__ __forceinline__ void update_path(uint32_t a)
+    {
+        const uint32_t k = update_fast(a);
+        if (k != 0xFFFFFFFFu) walk(lane_read(a, k));
     }
 };
 
@@ -488,59 +508,89 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
 
 // ------------------------------------------------------------------------- output stage --
 
-// Bits gather in a scalar accumulator and leave as big-endian dwords through a VGPR stage of
-// 64 words (one coalesced 256-byte buffer store). The u64 count (words 0-1) is rewritten at
-// the end by the same lanes that first stored them, so program order keeps it last.
-struct BitSink {
+// Code records: the encoder does not shift bits per symbol. Symbol t's code becomes one record
+// in lane t of a VGPR, 1 << len | code (len <= 31; the leading 1 marks the length), written with
+// one compare + select. Every 64 records (and at the end) pack() turns them into bytes on the
+// lanes: a DPP scan of the lengths gives each record its bit offset, each record ORs its head
+// (and the tail that spills into the next word) into a 64-word LDS stage, and the complete
+// words leave as one buffer store, big-endian. 64 records of <= 31 bits plus < 32 pending bits
+// fill at most 63 words. The u64 count (words 0-1) is written at the end by the lanes that
+// stored those words first, so program order keeps it last.
+struct RecSink {
     rsrc_t rs;
     uint32_t lane;
-    uint32_t wbase;  // word index of stage lane 0
-    uint32_t widx;   // next stage lane
-    uint32_t stage;
-    uint64_t acc;    // pending bits, MSB-aligned
-    uint32_t nacc;   // pending bit count, < 32 between calls
+    uint32_t *stage;  // the wave's 64 scratch words
+    uint32_t vrec;    // lane k: record k of the current group
+    uint32_t n;       // records in the group (outside the hot loop)
+    uint32_t pend;    // bits of the first unfinished output word, MSB-aligned
+    uint32_t nb;      // how many (< 32)
+    uint32_t wout;    // its word index
 
-    __device__ __forceinline__ void word(uint32_t w)
+    // inclusive prefix sum over the wave (row shifts, then row broadcasts 15 and 31)
+    static __device__ __forceinline__ uint32_t scan_add(uint32_t x)
     {
-        stage = lane == widx ? __builtin_bswap32(w) : stage;
-        if (++widx == 64) {
-            buf_store(rs, (wbase + lane) * 4, stage);
-            wbase += 64;
-            widx = 0;
-        }
+        x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+        x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+        x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+        x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+        x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false); // row_bcast:15
+        x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false); // row_bcast:31
+        return x;
     }
-    // append the n (1..32) low bits of x, MSB first
-    __device__ __forceinline__ void put(uint32_t x, uint32_t n)
+
+    // append record rec as number n of the group (outside the hot loop)
+    __device__ __forceinline__ void push(uint32_t rec)
     {
-        acc |= (uint64_t)x << (64 - nacc - n);
-        nacc += n;
-        if (nacc >= 32) {
-            word((uint32_t)(acc >> 32));
-            acc <<= 32;
-            nacc -= 32;
-        }
+        vrec = lane == n ? rec : vrec;
+        if (++n == 64) pack();
     }
-    __device__ __forceinline__ void put64(uint64_t x, uint32_t n)
+    // the low n (<= 64) bits of x, MSB first, as records of <= 24 bits
+    __device__ void push_bits(uint64_t x, uint32_t nbits)
     {
-        if (n > 32) {
-            put((uint32_t)(x >> 32), n - 32);
-            put((uint32_t)x, 32);
-        } else {
-            put((uint32_t)x, n);
+        while (nbits > 24) {
+            nbits -= 24;
+            push((1u << 24) | ((uint32_t)(x >> nbits) & 0xFFFFFFu));
         }
+        if (nbits) push((1u << nbits) | ((uint32_t)x & ((1u << nbits) - 1u)));
     }
-    // zero-pad to a byte (transform.cpp:379-381); store what is left; return the byte length
+
+    __device__ void pack()
+    {
+        const uint32_t rec = lane < n ? vrec : 0u;
+        const uint32_t len = rec ? 31u - (uint32_t)__builtin_clz(rec) : 0u;
+        const uint32_t code = rec & ((1u << len) - 1u);
+        const uint32_t msb = code << ((32u - len) & 31u);  // len 0: code 0
+        const uint32_t incl = scan_add(len);
+        const uint32_t p = nb + incl - len;  // bit offset in the group's words
+        const uint32_t w = p >> 5, o = p & 31u;
+        uint32_t head = msb >> o;
+        const uint32_t tail = o + len > 32u ? msb << (32u - o) : 0u;
+        head |= lane == 0 ? pend : 0u;
+        stage[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        __hip_atomic_fetch_or(&stage[w], head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_or(&stage[w + 1], tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t word = stage[lane];
+        const uint32_t total = nb + lane_read(incl, 63);
+        const uint32_t full = total >> 5;  // <= 62
+        buf_store(rs, lane < full ? (wout + lane) * 4 : kDrop, __builtin_bswap32(word));
+        pend = lane_read(word, full);
+        nb = total & 31u;
+        wout += full;
+        n = 0;
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // pack what is left, zero-pad to a byte (transform.cpp:379-381), store the last 0..4 bytes;
+    // returns the byte length
     __device__ __forceinline__ uint64_t finish()
     {
-        if (nacc & 7u) put(0, 8 - (nacc & 7u));
-        const uint32_t tail = nacc >> 3;  // 0..3 bytes pending
-        const uint32_t tw = (uint32_t)(acc >> 32);
-        // whole words of the stage, then the tail bytes from lane widx
-        buf_store(rs, lane < widx ? (wbase + lane) * 4 : kDrop, stage);
-        const uint32_t tb = (wbase + widx) * 4;
-        for (uint32_t b = 0; b < 3; ++b)
-            buf_store8(rs, lane == widx && b < tail ? tb + b : kDrop, tw >> (24 - 8 * b));
-        return (uint64_t)(wbase + widx) * 4 + tail;
+        if (n) pack();
+        const uint32_t tail = (nb + 7u) >> 3;  // 0..4 bytes
+        for (uint32_t b = 0; b < 4; ++b)
+            buf_store8(rs, lane == 0 && b < tail ? wout * 4 + b : kDrop, pend >> (24 - 8 * b));
+        return (uint64_t)wout * 4 + tail;
     }
 };
 
@@ -573,35 +623,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     }
 
     Fgk<kWide, false> fgk(trees[wv], lane);
-    BitSink sink;
+    RecSink sink;
     sink.rs = make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
     sink.lane = lane;
-    sink.wbase = 0;
-    sink.widx = 2;  // words 0-1: the u64 symbol count, written again at the end
-    sink.stage = 0;
-    sink.acc = 0;
-    sink.nacc = 0;
+    sink.stage = fgk.T.scratch;
+    sink.vrec = 0;
+    sink.n = 0;
+    // headers.cpp:118-122: the flags byte opens word 2 (words 0-1: the u64 symbol count,
+    // written at the end)
     const uint32_t flags = kSrc == SRC_SYMBOLS ? bt.flags : (kSrc == SRC_RAW_DIFF ? 0x80u : 0u);
-    sink.put(flags, 8);  // headers.cpp:118-122
+    sink.pend = flags << 24;
+    sink.nb = 8;
+    sink.wout = 2;
 
     const uint32_t n32 = (uint32_t)n;
     const rsrc_t rin = make_rsrc(bt.in + in_off, (n32 + 3u) & ~3u);
 
-    // transform.cpp:363-384: per symbol encode (path before update), then update. Positions
-    // stay in range by construction, so `bad` (a bug detector) is checked once per chunk.
+    // transform.cpp:363-384: per symbol encode (path before update), then update. A symbol
+    // whose root path is cached (the common case) takes the hot path, written so that its
+    // wave-uniform values stay in VGPRs (the scalar unit is shared by the CU's 32 waves): the
+    // symbol's path-cache row, the lane-parallel update, its record in lane t - koff. Anything
+    // else (a symbol not cached, or unseen) takes the miss path, which appends its records
+    // through the sink and re-bases koff. Positions stay in range by construction, so `bad` (a
+    // bug detector) is checked once per chunk.
     const uint8_t *const sb = reinterpret_cast<const uint8_t *>(fgk.T.syms);
-    auto code = [&](uint32_t t) {  // symbol t of the LDS buffer
-        const uint32_t sv = vreg(sb[t]);
-        const uint32_t ws = uni(fgk.T.where[sv]);
-        uint32_t s = ws & 1023u;
-        if (ws >> 10) {  // path cached (never for a fresh symbol)
-            uint32_t pv, bits;
-            const uint32_t d = fgk.pc_get((ws >> 10) - 1, pv, bits);
-            fgk.update_path(pv);
-            sink.put(bits, d);
-            return;
-        }
+    auto miss = [&](uint32_t sv) {
         const uint32_t sym = uni(sv);
+        uint32_t s = uni(fgk.T.where[sym]) & 1023u;
         const uint32_t fresh = s == 0;
         if (fresh) s = uni(fgk.split(sym));
         uint32_t pv;
@@ -609,15 +657,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         // bit k = code bit (position parity, left = even) of level k; read MSB first it is the
         // root-to-leaf code (the kRoot lanes are even)
         const uint64_t bits = ballot(pv & 1u);
-        fgk.pc_insert(sym, s, pv, d, (uint32_t)bits);
+        if (d <= kSlotDepth) fgk.pc_insert(sym, s, pv, d, (1u << d) | (uint32_t)bits);
         fgk.update_path(pv);
         if (fresh) {
             // the path starts at the new leaf, one level below the NYT whose code is sent
             // (huffman.cpp:44-50): drop that lowest bit, then 8 raw bits
-            if (d > 1) sink.put64(bits >> 1, d - 1);
-            sink.put(sym, 8);
+            sink.push_bits(bits >> 1, d - 1);
+            sink.push((1u << 8) | sym);
         } else {
-            sink.put64(bits, d);
+            sink.push_bits(bits, d);
+        }
+    };
+    // code symbols syms[0..ns) of the LDS buffer. The hot loop carries only vt, the records and
+    // the cache's reference bits: a miss or a failed leader test leaves it (what = 1 / 2) and
+    // is finished outside, so the compiler adds no copies of the rare paths' state per symbol.
+    auto code_all = [&](uint32_t ns) {
+        uint32_t t = 0;
+        while (t < ns) {
+            const uint32_t koff = t - sink.n;  // symbol t's record goes to lane t - koff
+            const uint32_t tend = min(ns, koff + 64);
+            const uint32_t vkey = lane + koff;
+            uint32_t vt = vreg(t);
+            uint32_t what = 0, wk = 0, sv = 0;
+            do {
+                sv = sb[vt];
+                const uint32_t e = fgk.T.where[sv] >> 10;
+                if (any(e == 0)) {
+                    what = 1;
+                    break;
+                }
+                uint32_t pv;
+                const uint32_t rec = fgk.pc_get(e, pv);
+                sink.vrec = vkey == vt ? rec : sink.vrec;
+                const uint32_t k = fgk.update_fast(pv);
+                vt = vreg(vt + 1);
+                if (k != 0xFFFFFFFFu) {
+                    what = 2;
+                    wk = lane_read(pv, k);
+                    break;
+                }
+            } while (any(vt < tend));
+            t = uni(vt);
+            if (what == 1) {
+                sink.n = t - koff;
+                miss(sv);
+                ++t;
+                continue;
+            }
+            if (what == 2) fgk.walk(wk);
+            sink.n = t - koff;
+            if (sink.n == 64) sink.pack();
         }
     };
 
@@ -631,21 +720,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
             fgk.T.syms[lane] = chunk;
             __builtin_amdgcn_wave_barrier();
-            for (uint32_t t = 0; t < m; ++t) code(t);
+            code_all(m);
             nsym += m;
             continue;
         }
         // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
         const uint32_t ns = rle_chunk<kSrc>(chunk, m, base + m == n32 ? 1u : 0u, cy, fgk.T.syms,
                                             fgk.scr32(), lane);
-        for (uint32_t t = 0; t < ns; ++t) code(t);
+        code_all(ns);
         nsym += ns;
     }
 
     const uint64_t total = sink.finish();
     const uint32_t st = fgk.bad ? (uint32_t)HC_ERR_DEVICE : (total <= cap ? 0u : (uint32_t)HC_ERR_CAPACITY);
-    // headers.cpp:110-116: u64 little-endian symbol count in words 0-1 (lanes 0 and 1 stored
-    // those words first, so this store is ordered after theirs)
+    // headers.cpp:110-116: u64 little-endian symbol count in words 0-1 (stored after every
+    // payload word by program order)
     buf_store(sink.rs, lane < 2 ? lane * 4 : kDrop, lane ? (uint32_t)(nsym >> 32) : (uint32_t)nsym);
     if (lane == 0) {
         bt.out_lens[sid] = fgk.bad ? 0 : total;
