@@ -36,6 +36,7 @@ constexpr int kWaves = 4;
 constexpr uint32_t kMaxBufBytes = 0x7FFFFF00u;  // per-stream limit of the 32-bit buffer offsets
 constexpr uint32_t kDrop = 0x7FFFFFF8u;         // buffer offset past every range: access dropped
 
+constexpr uint32_t kMissPos = kWords - 2;  // sentinel: w[kMissPos + 1] <= w[kMissPos], so it fails
 constexpr uint32_t kSlots = 16;     // encoder path cache: entries
 constexpr uint32_t kSlotDepth = 12; // deepest cached path
 constexpr uint32_t kRow = 16;       // u16 per cache entry
@@ -62,7 +63,10 @@ struct alignas(16) Tree {
     // [12] code record 1 << depth | code bits, [13] depth | valid << 5 | symbol << 8, [14..15]
     // unused. One lane-based
     // address reads a lane's position and (lane 0) the row's metadata.
-    alignas(16) uint16_t pc[kDec ? 2 : kSlots * kRow];
+    // row "entry -1" (where[] entry 0: not cached): level 0 at sentinel position kMissPos, whose
+    // leader test always fails at lane 0, so a miss leaves the hot loop like a failed update
+    alignas(16) uint16_t pc_miss[kDec ? 2 : kRow];
+    uint16_t pc[kDec ? 2 : kSlots * kRow];
     alignas(8) uint32_t syms[kDec ? 64 : kSymWords];  // MNP-5 symbols: encoder one chunk, decoder one block
     // decoder level tables: level j (1..8) at 2^j - 2 + prefix: position | depth << 10 where
     // the walk from the root along the prefix's bits stops
@@ -136,7 +140,7 @@ struct Fgk {
     uint32_t gen;      // decoder: generation of the level tables
     uint32_t stale;    // decoder: >= kRefresh = rebuild the level tables (a swap moved a position
                        // they walk through: += kRefresh; a lookup they left short: += 1)
-    const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow] (entry e's row = e - 1)
+    const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
         : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_ref(0), gen(0), stale(kRefresh),
@@ -151,6 +155,7 @@ struct Fgk {
         if (!kDec) {
             for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
             for (uint32_t i = lane; i < kSlots * kRow; i += 64) T.pc[i] = (i % kRow) < kSlotDepth ? 0xFFFF : 0;
+            if (lane < kRow) T.pc_miss[lane] = lane == 0 ? kMissPos : kRoot;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -166,11 +171,11 @@ struct Fgk {
     // ---- encoder path cache: root paths of recently coded symbols (tests/fgk_cache_model.py).
     // A path changes only when a swap moves a position on it; splits touch no symbol's path.
 
-    // hit: row of entry e (lane k < 12: position of level k, lanes >= d read kRoot padding);
-    // returns the row's code record (word 12, see RecSink) in an SGPR
-    __device__ __forceinline__ uint32_t pc_get(uint32_t e, uint32_t &pv)
+    // hit: pr = entry e's row as read lane-parallel at pc_lane[e * kRow] (lane k < 12: position
+    // of level k, kRoot padding from the depth on); the path to pv, returns the row's code
+    // record (word 12, see RecSink) in an SGPR
+    __device__ __forceinline__ uint32_t pc_use(uint32_t e, uint32_t pr, uint32_t &pv)
     {
-        const uint32_t pr = pc_lane[e * kRow];  // one lane-parallel read of the whole row
         pv = lane < kSlotDepth ? pr : kRoot;
         pc_ref = vreg(pc_ref | (1u << e));
         return lane_read(pr, kSlotDepth);
@@ -396,9 +401,11 @@ struct Fgk {
     // is heavier. The root lanes always lead (the sentinel above is heavier). Levels below the
     // first one that fails increment with one store; without a failure the root lanes bump the
     // root in the same store, otherwise the serial walk takes over (and bumps it at the end).
-    __device__ __forceinline__ uint32_t update_fast(uint32_t a)
+    template <class Ahead>
+    __device__ __forceinline__ uint32_t update_fast(uint32_t a, Ahead &&ahead)
     {
         const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1], w2 = T.wt[a + 2];
+        ahead();  // the caller's reads for later symbols go out behind these
         const uint32_t par = kWide ? (uint32_t)T.up[a] : (w0 & 1023u);
         const uint32_t nxt = a + 1 == par ? w2 : w1;
         const uint64_t fail = ballot(nxt <= (kWide ? w0 : (w0 | 1023u)));
@@ -409,7 +416,7 @@ struct Fgk {
     }
     __device__ __forceinline__ void update_path(uint32_t a)
     {
-        const uint32_t k = update_fast(a);
+        const uint32_t k = update_fast(a, [] {});
         if (k != 0xFFFFFFFFu) walk(lane_read(a, k));
     }
 };
@@ -668,9 +675,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
             sink.push_bits(bits, d);
         }
     };
-    // code symbols syms[0..ns) of the LDS buffer. The hot loop carries only vt, the records and
-    // the cache's reference bits: a miss or a failed leader test leaves it (what = 1 / 2) and
-    // is finished outside, so the compiler adds no copies of the rare paths' state per symbol.
+    // code symbols syms[0..ns) of the LDS buffer. The hot loop carries only vt, the records, the
+    // cache's reference bits and its read pipeline: a miss or a failed leader test leaves it
+    // (what = 1 / 2) and is finished outside, so the compiler adds no copies of the rare paths'
+    // state per symbol. Pipeline: while symbol t updates, the cache row of t+1, the where[]
+    // entry of t+2 and the byte of t+3 are already in flight. where[] and the rows change only
+    // on the paths that leave the loop (split, insert, swap), so what was read ahead stays
+    // valid inside it; the loop is re-primed after every exit. Bytes past ns are older symbols
+    // of the same buffer: their reads are harmless.
     auto code_all = [&](uint32_t ns) {
         uint32_t t = 0;
         while (t < ns) {
@@ -678,33 +690,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
             const uint32_t tend = min(ns, koff + 64);
             const uint32_t vkey = lane + koff;
             uint32_t vt = vreg(t);
-            uint32_t what = 0, wk = 0, sv = 0;
+            uint32_t ws0 = fgk.T.where[sb[vt]];      // where[] entry of symbol t
+            uint32_t ws1 = fgk.T.where[sb[vt + 1]];  // ... of t+1
+            uint32_t pr0 = fgk.pc_lane[(ws0 >> 10) * kRow];  // cache row of t (pc_miss if none)
+            uint32_t sv2 = sb[vt + 2];                       // byte of t+2
+            uint32_t e, pv, k;
             do {
-                sv = sb[vt];
-                const uint32_t e = fgk.T.where[sv] >> 10;
-                if (any(e == 0)) {
-                    what = 1;
-                    break;
-                }
-                uint32_t pv;
-                const uint32_t rec = fgk.pc_get(e, pv);
+                e = ws0 >> 10;
+                const uint32_t rec = fgk.pc_use(e, pr0, pv);
+                k = fgk.update_fast(pv, [&] {
+                    const uint32_t pr1 = fgk.pc_lane[(ws1 >> 10) * kRow];
+                    const uint32_t ws2 = fgk.T.where[sv2];
+                    const uint32_t sv3 = sb[vt + 3];
+                    ws0 = ws1;
+                    pr0 = pr1;
+                    ws1 = ws2;
+                    sv2 = sv3;
+                });
                 sink.vrec = vkey == vt ? rec : sink.vrec;
-                const uint32_t k = fgk.update_fast(pv);
                 vt = vreg(vt + 1);
-                if (k != 0xFFFFFFFFu) {
-                    what = 2;
-                    wk = lane_read(pv, k);
-                    break;
-                }
-            } while (any(vt < tend));
+            } while (k == 0xFFFFFFFFu && any(vt < tend));
             t = uni(vt);
-            if (what == 1) {
-                sink.n = t - koff;
-                miss(sv);
-                ++t;
-                continue;
+            if (k != 0xFFFFFFFFu) {
+                if (any(e == 0)) {  // not cached: nothing was written; code it from scratch
+                    --t;
+                    sink.n = t - koff;  // its record lane, overwritten by the miss path
+                    miss(sb[t]);
+                    ++t;
+                    continue;
+                }
+                fgk.walk(lane_read(pv, k));
             }
-            if (what == 2) fgk.walk(wk);
             sink.n = t - koff;
             if (sink.n == 64) sink.pack();
         }
