@@ -88,6 +88,13 @@ __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
+// lane l of v := x (x, l wave-uniform): the llvm.amdgcn.writelane intrinsic (no clang builtin in
+// this toolchain), so the compiler schedules it and handles its lane-select hazard
+__device__ int amdgcn_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t l)
+{
+    return (uint32_t)amdgcn_writelane((int)x, (int)l, (int)v);
+}
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ bool any(bool p) { return ballot(p) != 0; }
 // lowest set bit of a wave mask, 0xFFFFFFFF for 0 (s_ff1_i32_b64 without the zero test)
@@ -396,19 +403,20 @@ struct Fgk {
 
     // The same update when the path is already known: lanes 0..d-1 hold the positions of
     // levels 0..d-1, the other lanes kRoot. Until the first swap the tree does not change, so
-    // every level's leader test reads the pre-update words in parallel: a node leads its block
-    // when the next position is heavier, or when that position is its parent and the one after
-    // is heavier. The root lanes always lead (the sentinel above is heavier). Levels below the
-    // first one that fails increment with one store; without a failure the root lanes bump the
-    // root in the same store, otherwise the serial walk takes over (and bumps it at the end).
+    // every level's leader test reads the pre-update words in parallel. A level leads its block
+    // when the next position is heavier; the test cannot miss a non-leader, and it reports one
+    // falsely only when that next position is the level's own parent and the sibling weighs 0
+    // (the NYT): the walk, which repeats the exact test from the first reported level, handles
+    // both. The root lanes always lead (the sentinel above is heavier). Levels below the first
+    // reported one increment with one store; without a report the root lanes bump the root in
+    // the same store. update_fast() is this lane-parallel part; it returns the first reported
+    // level (0xFFFFFFFF: none), where walk() continues.
     template <class Ahead>
     __device__ __forceinline__ uint32_t update_fast(uint32_t a, Ahead &&ahead)
     {
-        const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1], w2 = T.wt[a + 2];
+        const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
         ahead();  // the caller's reads for later symbols go out behind these
-        const uint32_t par = kWide ? (uint32_t)T.up[a] : (w0 & 1023u);
-        const uint32_t nxt = a + 1 == par ? w2 : w1;
-        const uint64_t fail = ballot(nxt <= (kWide ? w0 : (w0 | 1023u)));
+        const uint64_t fail = ballot(w1 <= (kWide ? w0 : (w0 | 1023u)));
         const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
         *(lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
         __builtin_amdgcn_wave_barrier();
@@ -686,43 +694,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     auto code_all = [&](uint32_t ns) {
         uint32_t t = 0;
         while (t < ns) {
-            const uint32_t koff = t - sink.n;  // symbol t's record goes to lane t - koff
-            const uint32_t tend = min(ns, koff + 64);
-            const uint32_t vkey = lane + koff;
+            uint32_t rl = sink.n;  // record lane of symbol t (scalar)
+            const uint32_t rend = min(64u, rl + (ns - t));
             uint32_t vt = vreg(t);
-            uint32_t ws0 = fgk.T.where[sb[vt]];      // where[] entry of symbol t
-            uint32_t ws1 = fgk.T.where[sb[vt + 1]];  // ... of t+1
-            uint32_t pr0 = fgk.pc_lane[(ws0 >> 10) * kRow];  // cache row of t (pc_miss if none)
-            uint32_t sv2 = sb[vt + 2];                       // byte of t+2
+            uint32_t ws0 = vreg(fgk.T.where[sb[vt]]);      // where[] entry of symbol t
+            uint32_t ws1 = vreg(fgk.T.where[sb[vt + 1]]);  // ... of t+1
+            uint32_t e0 = ws0 >> 10;
+            uint32_t pr0 = vreg(fgk.pc_lane[e0 * kRow]);   // cache row of t (pc_miss if none)
+            uint32_t sv2 = vreg(sb[vt + 2]);               // byte of t+2
             uint32_t e, pv, k;
             do {
-                e = ws0 >> 10;
+                e = e0;
                 const uint32_t rec = fgk.pc_use(e, pr0, pv);
                 k = fgk.update_fast(pv, [&] {
-                    const uint32_t pr1 = fgk.pc_lane[(ws1 >> 10) * kRow];
+                    const uint32_t e1 = ws1 >> 10;
+                    const uint32_t pr1 = fgk.pc_lane[e1 * kRow];
                     const uint32_t ws2 = fgk.T.where[sv2];
                     const uint32_t sv3 = sb[vt + 3];
-                    ws0 = ws1;
+                    e0 = e1;
                     pr0 = pr1;
                     ws1 = ws2;
                     sv2 = sv3;
                 });
-                sink.vrec = vkey == vt ? rec : sink.vrec;
+                sink.vrec = writelane(sink.vrec, rec, rl);
                 vt = vreg(vt + 1);
-            } while (k == 0xFFFFFFFFu && any(vt < tend));
-            t = uni(vt);
+                ++rl;
+            } while (k == 0xFFFFFFFFu && rl < rend);
+            t += rl - sink.n;
             if (k != 0xFFFFFFFFu) {
                 if (any(e == 0)) {  // not cached: nothing was written; code it from scratch
                     --t;
-                    sink.n = t - koff;  // its record lane, overwritten by the miss path
+                    sink.n = rl - 1;  // its record lane, overwritten by the miss path
                     miss(sb[t]);
                     ++t;
                     continue;
                 }
                 fgk.walk(lane_read(pv, k));
             }
-            sink.n = t - koff;
-            if (sink.n == 64) sink.pack();
+            sink.n = rl;
+            if (rl == 64) sink.pack();
         }
     };
 
