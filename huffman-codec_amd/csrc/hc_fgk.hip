@@ -141,16 +141,15 @@ struct Fgk {
     uint32_t lane;
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
-    uint32_t pc_next;  // encoder: clock hand of the path cache
-    uint32_t pc_ref;   // encoder: reference bits of the entries (bit e + 1 = entry e), kept in a
-                       // VGPR: a hit sets its bit on the VALU
+    uint32_t pc_next;  // encoder: FIFO hand of the path cache
+    uint32_t pc_free;  // encoder: entries dropped by swaps (or never used), taken first
     uint32_t gen;      // decoder: generation of the level tables
     uint32_t stale;    // decoder: >= kRefresh = rebuild the level tables (a swap moved a position
                        // they walk through: += kRefresh; a lookup they left short: += 1)
     const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
-        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_ref(0), gen(0), stale(kRefresh),
+        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), gen(0), stale(kRefresh),
           pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
@@ -184,7 +183,6 @@ struct Fgk {
     __device__ __forceinline__ uint32_t pc_use(uint32_t e, uint32_t pr, uint32_t &pv)
     {
         pv = lane < kSlotDepth ? pr : kRoot;
-        pc_ref = vreg(pc_ref | (1u << e));
         return lane_read(pr, kSlotDepth);
     }
 
@@ -198,21 +196,20 @@ struct Fgk {
     }
 
     // after a miss: cache symbol sym at position s with its path (lanes >= d hold kRoot) and
-    // its code record rec (1 << d | code bits). The clock hand skips (and clears) referenced
-    // entries.
+    // its code record rec (1 << d | code bits). Replacement: an entry dropped by a swap (or
+    // never used) first, lowest number; otherwise FIFO (tests/fgk_cache_model.py: on the photo
+    // streams this misses less than a clock with reference bits, and a hit costs nothing).
     __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t rec)
     {
         if (d > kSlotDepth) return;
-        const uint32_t h = pc_next;
-        uint32_t ref = uni(pc_ref) >> 1;
-        const uint32_t rot = ((ref >> h) | (ref << (kSlots - h))) & 0xFFFFu;
-        const uint32_t k = rot == 0xFFFFu ? 0u : (uint32_t)__builtin_ctz(~rot);
-        const uint32_t passed = rot == 0xFFFFu ? 0xFFFFu : ((1u << k) - 1u);
-        const uint32_t e = (h + k) & (kSlots - 1);
-        ref &= ~(((passed << h) | (passed >> (kSlots - h))) & 0xFFFFu);
-        ref |= 1u << e;
-        pc_ref = vreg(ref << 1);
-        pc_next = (e + 1) & (kSlots - 1);
+        uint32_t e;
+        if (pc_free) {
+            e = (uint32_t)__builtin_ctz(pc_free);
+            pc_free &= pc_free - 1;
+        } else {
+            e = pc_next;
+            pc_next = (e + 1) & (kSlots - 1);
+        }
         // lane 0: the evicted symbol forgets its entry; lane 1: this symbol takes it
         pc_forget(e, lane == 1 ? &T.where[sym] : scr16(), s | ((e + 1) << 10));
         // lanes 0..11 the positions, 12 the code record, 13 depth | valid | symbol
@@ -226,7 +223,7 @@ struct Fgk {
         pc_forget(e, scr16(), 0);
         *(lane < kSlotDepth + 2 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)(lane < kSlotDepth ? 0xFFFFu : 0u);
         __builtin_amdgcn_wave_barrier();
-        pc_ref = vreg(pc_ref & ~(2u << e));
+        pc_free |= 1u << e;
     }
 
     // positions s and l traded contents: drop every cached path through either. Per read,

@@ -5,7 +5,8 @@ The slot-form tree (oracle/hc_oracle.c: sl_*) changes shape 
 places, huffman.cpp:186-217). Two caches exploit that:
 
 * path cache (encoder): the root paths (positions, code bits) of up to 16 recently coded
-  symbols whose paths are at most 12 deep, clock replacement. A swap of s and lead stales exactly the cached paths that contain s or
+  symbols whose paths are at most 12 deep; a new path takes an entry dropped by a swap (or
+  never used) first, else the FIFO hand's. A swap of s and lead stales exactly the cached paths that contain s or
   lead; a split stales none (the NYT position is on no symbol's path).
 * level tables (decoder): for j = 1..8 and each j-bit prefix, the position reached from the root
   by reading the prefix's bits (stopping at a leaf). The 8-bit table finds the leaf; lane 64-j
@@ -88,14 +89,12 @@ class Tree:
 
 
 class PathCache:
-    """Clock replacement (second chance), as the kernel: a hit sets the entry's reference
-    bit; an insert takes the first entry from `next` on whose bit is clear, clearing the bits
-    it passes (all of them when every bit is set); dropping an entry clears its bit."""
+    """As the kernel: an insert takes the lowest-numbered free entry (dropped by a swap, or
+    never used), else the entry at the FIFO hand `next`; a hit changes nothing."""
 
     def __init__(self):
         self.ent = [None] * SLOTS  # (sym, pv)
         self.slot = {}             # sym -> slot
-        self.ref = 0               # reference bits
         self.next = 0
         self.hits = self.misses = self.inval = 0
 
@@ -105,22 +104,18 @@ class PathCache:
             self.misses += 1
             return None
         self.hits += 1
-        self.ref |= 1 << e
         return self.ent[e][1]
 
     def insert(self, sym, pv):
         if len(pv) > MAXD:
             return
-        k = 0
-        while k < SLOTS and self.ref >> ((self.next + k) % SLOTS) & 1:
-            k += 1
-        if k == SLOTS:
-            self.ref, k = 0, 0
-        for j in range(k):
-            self.ref &= ~(1 << ((self.next + j) % SLOTS))
-        e = (self.next + k) % SLOTS
-        self.next = (e + 1) % SLOTS
-        self.ref |= 1 << e
+        # an entry dropped by a swap (or never used) first, lowest number; otherwise FIFO
+        free = [e for e in range(SLOTS) if self.ent[e] is None]
+        if free:
+            e = free[0]
+        else:
+            e = self.next
+            self.next = (e + 1) % SLOTS
         if self.ent[e] is not None:
             self.slot.pop(self.ent[e][0], None)
         self.ent[e] = (sym, list(pv))
@@ -131,7 +126,6 @@ class PathCache:
             if self.ent[e] is not None and (s in self.ent[e][1] or lead in self.ent[e][1]):
                 self.slot.pop(self.ent[e][0], None)
                 self.ent[e] = None
-                self.ref &= ~(1 << e)
                 self.inval += 1
 
 
