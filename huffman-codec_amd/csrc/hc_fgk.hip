@@ -25,6 +25,10 @@
 //    stage and leave as one coalesced 256-byte buffer store per 64 words.
 #include "hc_internal.h"
 
+// llvm.amdgcn.writelane has no clang builtin in this toolchain; binding the intrinsic by name
+// lets the compiler schedule it and handle its lane-select hazard (unlike inline asm)
+extern "C" __device__ int amdgcn_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
+
 namespace hc {
 namespace {
 
@@ -88,9 +92,7 @@ __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
-// lane l of v := x (x, l wave-uniform): the llvm.amdgcn.writelane intrinsic (no clang builtin in
-// this toolchain), so the compiler schedules it and handles its lane-select hazard
-__device__ int amdgcn_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
+// lane l of v := x (x, l wave-uniform): the llvm.amdgcn.writelane intrinsic (declared above)
 __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t l)
 {
     return (uint32_t)amdgcn_writelane((int)x, (int)l, (int)v);
