@@ -73,7 +73,9 @@ struct alignas(16) Tree {
     uint16_t pc[kDec ? 2 : kSlots * kRow];
     alignas(8) uint32_t syms[kDec ? 64 : kSymWords];  // MNP-5 symbols: encoder one chunk, decoder one block
     // decoder level tables: level j (1..8) at 2^j - 2 + prefix: position | depth << 10 where
-    // the walk from the root along the prefix's bits stops
+    // the walk from the root along the prefix's bits stops; lvl_root (indices -2, -1: "level
+    // 0") holds the root, which the lanes above a path's depth read
+    uint16_t lvl_root[2];
     uint16_t lvl[kDec ? 512 : 2];
 };
 
@@ -156,6 +158,7 @@ struct Fgk {
     {
         // huffman.cpp:23-31: a lone NYT root
         for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
+        if (lane < 2) T.lvl_root[lane] = kRoot;
         for (uint32_t i = lane; i < 516; i += 64) {
             T.body[i] = i == kRoot ? kNyt : 0;
             if (kWide) T.up[i] = 0;
@@ -410,12 +413,14 @@ struct Fgk {
     // reported one increment with one store; without a report the root lanes bump the root in
     // the same store. update_fast() is this lane-parallel part; it returns the first reported
     // level (0xFFFFFFFF: none), where walk() continues.
+    // force (wave-uniform, 0 or 0 - 1 / 0 - 2 / 0 - 3): report level 0, store nothing (the
+    // limit becomes all ones, above every weight word and sentinel)
     template <class Ahead>
-    __device__ __forceinline__ uint32_t update_fast(uint32_t a, Ahead &&ahead)
+    __device__ __forceinline__ uint32_t update_fast(uint32_t a, Ahead &&ahead, uint32_t force = 0)
     {
         const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
         ahead();  // the caller's reads for later symbols go out behind these
-        const uint64_t fail = ballot(w1 <= (kWide ? w0 : (w0 | 1023u)));
+        const uint64_t fail = ballot(w1 <= (kWide ? (w0 | force | (force >> 1)) : (w0 | 1023u | force)));
         const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
         *(lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
         __builtin_amdgcn_wave_barrier();
@@ -769,27 +774,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
 
 // --------------------------------------------------------------------------- the decoder --
 
-// MSB-first reader over a stream's bytes; words come from a 64-word VGPR chunk.
+// MSB-first reader over a stream's bytes; words come from a 64-word VGPR chunk, the next chunk
+// already loading (its wait falls ~64 refills later).
 struct BitSource {
     rsrc_t rs;
     uint32_t lane;
     uint32_t cbase;  // byte offset of chunk lane 0
     uint32_t chunk;  // big-endian words (byte-swapped once per load, on the lanes)
+    uint32_t nxt;    // the following 256 bytes as loaded
     uint32_t ridx;
     uint64_t win;  // upcoming bits, MSB-aligned
     uint32_t nwin; // valid bits in win
 
+    __device__ __forceinline__ void next_word()
+    {
+        if (++ridx == 64) {
+            cbase += 256;
+            chunk = __builtin_bswap32(nxt);
+            nxt = buf_load(rs, cbase + 256 + lane * 4);
+            ridx = 0;
+        }
+    }
     // push the next 32 bits (needs nwin <= 32)
     __device__ __forceinline__ void refill()
     {
         const uint32_t w = lane_read(chunk, ridx);
         win |= (uint64_t)w << (32 - nwin);
         nwin += 32;
-        if (++ridx == 64) {
-            cbase += 256;
-            chunk = __builtin_bswap32(buf_load(rs, cbase + lane * 4));
-            ridx = 0;
-        }
+        next_word();
     }
     __device__ __forceinline__ uint32_t bit()
     {
@@ -938,6 +950,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     in.lane = lane;
     in.cbase = 0;
     in.chunk = __builtin_bswap32(hdr);
+    in.nxt = buf_load(rin, 256 + lane * 4);
     in.ridx = 2;
     in.win = 0;
     in.nwin = 0;
@@ -963,68 +976,79 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     for (uint32_t i0 = 0; i0 < n; i0 += 256) {
         if (fgk.bad || pos > kMaxBufBytes || consumed() > payload_bits + 64) break;
         const uint32_t i1 = min(n, i0 + 256);
-        for (uint32_t i = i0; i < i1; ++i) {
+        uint32_t i = i0;
+        while (i < i1) {
             // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
             // where the walk from the root stops (depth d <= 8); lane k < d reads level d-k's
-            // entry for the same prefix, the position of path level k (0 = the leaf). Codes
-            // longer than the tables reach go on bit by bit over a window of >= 33 bits.
+            // entry for the same prefix, the position of path level k (0 = the leaf).
             if (fgk.stale >= kRefresh) fgk.build_levels();
             if (in.nwin <= 32) in.refill();
-            const uint32_t v = (uint32_t)(in.win >> 56);
-            const uint32_t e8 = uni(fgk.T.lvl[254 + v]);
-            uint32_t x = e8 & 1023u, depth = e8 >> 10;
-            uint32_t b = uni(fgk.T.body[x]);
-            uint32_t pv;
-            if (!(b & kInner)) {
-                // level j's entry for prefix v >> (8 - j) sits at 2^j - 2 + (v >> (8 - j))
-                // = ((256 | v) >> (8 - j)) - 2; lane k needs j = depth - k (idle lanes: any)
-                const uint32_t sh = min(8 - depth + lane, 7u);
-                pv = fgk.T.lvl[((256u | v) >> sh) - 2] & 1023u;
-                pv = lane < depth ? pv : kRoot;
-                in.win <<= depth;
-                in.nwin -= depth;
-            } else {  // top-down first (depth j at lane 64-j), then turned bottom-up
+            // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
+            // symbol's depth is known the next symbol's table entry is read, before this
+            // symbol's update (the tables and body[] change only on the paths that leave the
+            // loop, and the loop is re-entered after them). Anything else
+            // (a longer code or a stale table: body inner; the NYT; a failed leader test) is
+            // forced to fail at level 0 so nothing is stored, and is finished outside.
+            const uint32_t lane8 = min(lane + 8, 31u);  // lane k: shift for level d - k
+            uint32_t e8 = uni(fgk.T.lvl[(uint32_t)(in.win >> 56) + 254]);
+            uint32_t v, d, x, b, pv, k;
+            do {
+                v = (uint32_t)(in.win >> 56);
+                x = e8 & 1023u;
+                d = e8 >> 10;
+                b = fgk.T.body[x];
+                // level j's entry for prefix v >> (8 - j) sits at ((256 | v) >> (8 - j)) - 2;
+                // lane k needs j = d - k; lanes k >= d shift by >= 8 and read lvl_root
+                const uint32_t pr = fgk.T.lvl[((256u | v) >> (lane8 - d)) - 2];
+                in.win <<= d;
+                in.nwin -= d;  // >= 25
+                const uint32_t e8n = fgk.T.lvl[(uint32_t)(in.win >> 56) + 254];  // next symbol
+                pv = pr & 1023u;
+                // a leaf's body is its symbol; inner / NYT (bits 8, 9): force the failure
+                const uint32_t force = 0u - __builtin_amdgcn_ubfe(b, 8, 2);
+                k = fgk.update_fast(pv, [] {}, force);
+                sbuf[i - i0] = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
+                ++i;
+                if (in.nwin <= 32) in.refill();
+                e8 = uni(e8n);
+            } while (k == 0xFFFFFFFFu && i < i1);
+            if (k == 0xFFFFFFFFu) continue;
+            // symbol i - 1 left the loop: the window stands d bits into its code
+            b = uni(b);
+            if (!(b & (kInner | kNyt))) {  // a leaf whose update reported level k: walk from there
+                fgk.walk(lane_read(pv, k));
+                continue;
+            }
+            // nothing was stored for it
+            uint32_t sym = 0;
+            if (b & kInner) {
+                // the code is longer than the tables reach, or they stopped short (a leaf that
+                // split since): descend bit by bit, top-down first (depth j at lane 64-j),
+                // then turned bottom-up
+                uint32_t depth = uni(d);
+                x = uni(x);
                 fgk.stale += depth < 8 ? 1u : 0u;
                 const uint32_t jl = 64 - lane, jc = jl > 8 ? 8 : jl;
-                uint32_t pt = fgk.T.lvl[(1u << jc) - 2 + (v >> (8 - jc))] & 1023u;
-                uint64_t w = in.win << depth;
+                uint32_t pt = fgk.T.lvl[(1u << jc) - 2 + (uni(v) >> (8 - jc))] & 1023u;
                 do {
-                    x = min((b & 255u) * 2 + (uint32_t)(w >> 63), x - 1);  // children sit below
-                    w <<= 1;
+                    x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
                     pt = lane == 63 - depth ? x : pt;
                     ++depth;
                     b = uni(fgk.T.body[x]);
-                } while (b & kInner);
-                if (depth > in.nwin) {  // a code longer than the window (deep trees only)
-                    x = kRoot;
-                    depth = 0;
-                    b = uni(fgk.T.body[kRoot]);
-                    while (b & kInner) {
-                        x = min((b & 255u) * 2 + in.bit(), x - 1);
-                        pt = lane == 63 - depth ? x : pt;
-                        ++depth;
-                        b = uni(fgk.T.body[x]);
-                    }
-                } else {
-                    in.win = w;
-                    in.nwin -= depth;
-                }
+                } while ((b & kInner) && depth < 63);
                 if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
                 pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
                 pv = lane < depth ? pv : kRoot;
+                sym = b & 255u;
             }
-            uint32_t sym;
             if (b & kNyt) {  // the new leaf below the NYT becomes level 0
                 sym = in.bits8();
                 x = uni(fgk.split(sym));
                 pv = __shfl_up(pv, 1, 64);
                 pv = lane == 0 ? x : pv;
-            } else {
-                sym = b & 255u;
             }
-            fgk.update_path(pv);
-
-            sbuf[i - i0] = (uint8_t)sym;  // every lane stores the same byte
+            if (!(b & kInner)) fgk.update_path(pv);
+            sbuf[i - 1 - i0] = (uint8_t)sym;
         }
         __builtin_amdgcn_wave_barrier();
         const uint32_t x4 = fgk.T.syms[lane];
