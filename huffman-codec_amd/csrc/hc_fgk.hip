@@ -30,7 +30,39 @@
 extern "C" __device__ int amdgcn_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
 
 namespace hc {
+
+// Diagnostic: when non-null, every FGK wave records (start, end, HW_ID | XCC_ID << 16) at
+// [3 * stream] (scripts/residency.py measures how many waves share each SIMD). Set by
+// hc_debug_set_trace (not part of include/hcodec.h); null in normal use.
+__device__ uint64_t *g_trace = nullptr;
+
 namespace {
+
+__device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t lane)
+{
+    uint64_t *const tr = g_trace;
+    if (tr == nullptr) return;
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0) {
+        tr[3 * sid] = t0;
+        tr[3 * sid + 1] = t1;
+        tr[3 * sid + 2] = (hw & 0xFFFFu) | ((xcc & 0xFu) << 16);
+    }
+}
+
+// The issue arbiter prefers higher priority, then older waves: left alone, the oldest of a
+// SIMD's 8 waves run ahead and the last ones finish long after, on a half-empty SIMD. Waves
+// that are behind (by the quarter of their stream done) take a higher priority instead.
+__device__ __forceinline__ void prio_by_progress(uint32_t done, uint32_t total)
+{
+    if ((uint64_t)done * 4 < total) __builtin_amdgcn_s_setprio(3);
+    else if ((uint64_t)done * 2 < total) __builtin_amdgcn_s_setprio(2);
+    else if ((uint64_t)done * 4 < 3ull * total) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 
 constexpr uint32_t kRoot = 512;
 constexpr uint32_t kWords = 576;  // positions 0..512 + sentinels 513..575 (s + 63)
@@ -619,6 +651,7 @@ template <bool kWide, int kSrc>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void encode_kernel(Batch bt)
 {
     __shared__ Tree<kWide, false> trees[kWaves];
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
@@ -744,6 +777,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     uint32_t next = buf_load(rin, lane * 4);
     RleCarry cy = {0, 0, 0};
     for (uint32_t base = 0; base < n32 && !fgk.bad; base += 256) {
+        prio_by_progress(base, n32);
         const uint32_t chunk = next;
         next = buf_load(rin, base + 256 + lane * 4);  // out of range past the end: reads 0
         const uint32_t m = min(256u, n32 - base);
@@ -770,6 +804,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         bt.out_lens[sid] = fgk.bad ? 0 : total;
         bt.status[sid] = (int32_t)st;
     }
+    trace_wave(sid, t0, lane);
 }
 
 // --------------------------------------------------------------------------- the decoder --
@@ -908,6 +943,7 @@ template <bool kWide, int kDst>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void decode_kernel(Batch bt)
 {
     __shared__ Tree<kWide, true> trees[kWaves];
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
@@ -975,6 +1011,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
 
     for (uint32_t i0 = 0; i0 < n; i0 += 256) {
         if (fgk.bad || pos > kMaxBufBytes || consumed() > payload_bits + 64) break;
+        prio_by_progress(i0, n);
         const uint32_t i1 = min(n, i0 + 256);
         uint32_t i = i0;
         while (i < i1) {
@@ -1069,6 +1106,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
         bt.status[sid] = (int32_t)st;
         bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? pos : 0;
     }
+    trace_wave(sid, t0, lane);
 }
 
 }  // namespace
@@ -1109,3 +1147,9 @@ hipError_t launch_decode(const Batch &b, DecDst dst, hipStream_t st)
 }
 
 }  // namespace hc
+
+extern "C" int hc_debug_set_trace(void *dev_buf)
+{
+    uint64_t *p = static_cast<uint64_t *>(dev_buf);
+    return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_trace), &p, sizeof(p)) == hipSuccess ? 0 : HC_ERR_DEVICE;
+}

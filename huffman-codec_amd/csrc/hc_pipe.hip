@@ -1,0 +1,311 @@
+// hc_pipe.hip — host-buffer batches: many independent streams that live in host memory
+// (files), pushed through the batched device coder in pipelined sub-batches (SURVEY.md §8f-1;
+// the reference codes one file per process, main.cpp:202-220).
+//
+// Per sub-batch, on its own HIP stream: the inputs are packed into pinned staging (host
+// memcpy), copied up, coded by the fused FGK kernels, then compacted on the device (each
+// stream's bytes moved next to the previous stream's) so that only the produced bytes cross
+// PCIe. Two slots alternate, so one sub-batch's kernels run while the previous one's results
+// come back and are unpacked into the caller's buffers, and while the next one is staged.
+// A stream whose output outgrows the sub-batch's device capacity guess reports the exact size
+// and is coded again on its own.
+#include <string.h>
+
+#include <hipcub/hipcub.hpp>
+#include <vector>
+
+#include "hc_internal.h"
+
+namespace {
+
+#define PIPE_CK(x)                                     \
+    do {                                               \
+        if ((x) != hipSuccess) return HC_ERR_DEVICE;   \
+    } while (0)
+
+constexpr uint64_t kAlign = 16;
+uint64_t up16(uint64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// length of the produced bytes that travel back (failed streams: none)
+__global__ void kept_lengths(const uint64_t *lens, const int32_t *status, uint64_t *kept, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) kept[i] = status[i] == 0 ? lens[i] : 0;
+}
+
+// stream i's kept bytes from out + offs[i] to packed + at[i]; one workgroup per stream
+__global__ __launch_bounds__(256) void compact(const uint8_t *out, const uint64_t *offs, const uint64_t *kept,
+                                               const uint64_t *at, uint8_t *packed)
+{
+    const uint32_t i = blockIdx.x;
+    const uint8_t *src = out + offs[i];
+    uint8_t *dst = packed + at[i];
+    const uint64_t len = kept[i];
+    for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) dst[k] = src[k];
+}
+
+template <class T>
+struct Dev {
+    T *p = nullptr;
+    uint64_t cap = 0;
+    ~Dev() { if (p) (void)hipFree(p); }
+    hipError_t need(uint64_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const hipError_t e = hipMalloc(&p, (n ? n : 1) * sizeof(T));
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+};
+
+template <class T>
+struct Pinned {
+    T *p = nullptr;
+    uint64_t cap = 0;
+    ~Pinned() { if (p) (void)hipHostFree(p); }
+    hipError_t need(uint64_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const hipError_t e = hipHostMalloc(&p, (n ? n : 1) * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+};
+
+// meta words per stream, uploaded / downloaded as one block: in_off, in_len, out_off, out_cap
+// (up); out_len, status, kept offset (down)
+struct Slot {
+    hipStream_t st = nullptr;
+    hipEvent_t meta_done = nullptr;
+    Pinned<uint8_t> hin, hpacked;
+    Pinned<uint64_t> hup, hdown;
+    Dev<uint8_t> din, dout, dpacked, dtmp;
+    Dev<uint64_t> dup, dlens, dkept, dat;
+    Dev<int32_t> dstatus;
+    uint32_t first = 0, count = 0;  // streams [first, first + count) of the call
+    bool busy = false;
+    ~Slot()
+    {
+        if (meta_done) (void)hipEventDestroy(meta_done);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+struct Job {
+    bool encode;
+    uint32_t flags;
+    const uint8_t *const *in;
+    const uint64_t *in_lens;
+    uint8_t *const *out;
+    const uint64_t *out_caps;
+    uint64_t *out_lens;
+    int32_t *status;
+    std::vector<uint64_t> dcap;  // device capacity per stream (a guess for decode)
+};
+
+// device capacity for stream i: encode — the input plus a quarter (FGK rarely expands data
+// more; a stream that does reports its exact size and is redone); decode — the same idea
+// against the header's symbol count (RLE expands 4 symbols to at most 258 bytes)
+uint64_t guess_cap(const Job &j, uint32_t i)
+{
+    const uint64_t n = j.in_lens[i];
+    uint64_t c;
+    if (j.encode) {
+        c = n + n / 4 + 4096;
+    } else {
+        uint64_t count = 0;
+        if (n >= 9)
+            for (int b = 7; b >= 0; --b) count = (count << 8) | j.in[i][b];
+        const uint64_t most = count * 65 + 8;
+        c = n * 8 > 65536 ? n * 8 : 65536;
+        if (c > most) c = most;
+    }
+    return c < j.out_caps[i] ? c : j.out_caps[i];
+}
+
+int launch(Job &j, Slot &s)
+{
+    const uint32_t n = s.count;
+    uint64_t in_bytes = 0, out_bytes = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        in_bytes += up16(j.in_lens[s.first + k]);
+        out_bytes += up16(j.dcap[s.first + k]);
+    }
+    PIPE_CK(s.hin.need(in_bytes));
+    PIPE_CK(s.hup.need(4ull * n));
+    PIPE_CK(s.hdown.need(3ull * n + 1));
+    PIPE_CK(s.din.need(in_bytes));
+    PIPE_CK(s.dout.need(out_bytes));
+    PIPE_CK(s.dpacked.need(out_bytes));
+    PIPE_CK(s.dup.need(4ull * n));
+    PIPE_CK(s.dlens.need(n));
+    PIPE_CK(s.dkept.need(n));
+    PIPE_CK(s.dat.need(n + 1));
+    PIPE_CK(s.dstatus.need(n));
+    // stage: inputs packed at 16-byte aligned offsets, meta columns
+    uint64_t *up = s.hup.p;
+    uint64_t io = 0, oo = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t i = s.first + k;
+        const uint64_t len = j.in_lens[i];
+        if (len) memcpy(s.hin.p + io, j.in[i], len);
+        up[k] = io;
+        up[n + k] = len;
+        up[2 * n + k] = oo;
+        up[3 * n + k] = j.dcap[i];
+        io += up16(len);
+        oo += up16(j.dcap[i]);
+    }
+    PIPE_CK(hipMemcpyAsync(s.din.p, s.hin.p, in_bytes, hipMemcpyHostToDevice, s.st));
+    PIPE_CK(hipMemcpyAsync(s.dup.p, up, 4ull * n * sizeof(uint64_t), hipMemcpyHostToDevice, s.st));
+    const uint64_t *d = s.dup.p;
+    hc::Batch b{s.din.p, d, d + n, n, s.dout.p, d + 2 * n, d + 3 * n, s.dlens.p, s.dstatus.p, j.flags};
+    if (j.encode)
+        PIPE_CK(hc::launch_encode(b, (j.flags & HC_FLAG_DIFF) ? hc::SRC_RAW_DIFF : hc::SRC_RAW, s.st));
+    else
+        PIPE_CK(hc::launch_decode(b, hc::DST_RAW, s.st));
+    // compaction: kept lengths, their exclusive scan (+ total), the copy
+    kept_lengths<<<(n + 255) / 256, 256, 0, s.st>>>(s.dlens.p, s.dstatus.p, s.dkept.p, n);
+    size_t tb = 0;
+    PIPE_CK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s.dkept.p, s.dat.p, (int)n, s.st));
+    PIPE_CK(s.dtmp.need(tb));
+    PIPE_CK(hipcub::DeviceScan::ExclusiveSum(s.dtmp.p, tb, s.dkept.p, s.dat.p, (int)n, s.st));
+    compact<<<n, 256, 0, s.st>>>(s.dout.p, d + 2 * n, s.dkept.p, s.dat.p, s.dpacked.p);
+    PIPE_CK(hipGetLastError());
+    PIPE_CK(hipMemcpyAsync(s.hdown.p, s.dlens.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s.st));
+    PIPE_CK(hipMemcpyAsync(s.hdown.p + n, s.dat.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s.st));
+    PIPE_CK(hipMemcpyAsync(s.hdown.p + 2 * n, s.dstatus.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, s.st));
+    PIPE_CK(hipEventRecord(s.meta_done, s.st));
+    s.busy = true;
+    return HC_OK;
+}
+
+// results of slot s: wait for its meta, bring the packed bytes, unpack into the caller's buffers
+int finish(Job &j, Slot &s, std::vector<uint32_t> &redo)
+{
+    const uint32_t n = s.count;
+    PIPE_CK(hipEventSynchronize(s.meta_done));
+    const uint64_t *lens = s.hdown.p, *at = s.hdown.p + n;
+    const int32_t *st = reinterpret_cast<const int32_t *>(s.hdown.p + 2 * n);
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < n; ++k)
+        if (st[k] == 0) total = at[k] + lens[k];
+    PIPE_CK(s.hpacked.need(total));
+    if (total) {
+        PIPE_CK(hipMemcpyAsync(s.hpacked.p, s.dpacked.p, total, hipMemcpyDeviceToHost, s.st));
+        PIPE_CK(hipStreamSynchronize(s.st));
+    }
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t i = s.first + k;
+        j.out_lens[i] = lens[k];
+        j.status[i] = st[k];
+        if (st[k] == 0) {
+            if (lens[k]) memcpy(j.out[i], s.hpacked.p + at[k], lens[k]);
+        } else if (st[k] == HC_ERR_CAPACITY && j.dcap[i] < j.out_caps[i]) {
+            // the guess was short: code it again with what it needs (or all the caller has)
+            j.dcap[i] = lens[k] < j.out_caps[i] ? lens[k] : j.out_caps[i];
+            redo.push_back(i);
+        }
+    }
+    s.busy = false;
+    return HC_OK;
+}
+
+uint64_t env_u64(const char *name, uint64_t dflt)
+{
+    const char *v = getenv(name);
+    if (!v || !*v) return dflt;
+    const uint64_t x = strtoull(v, nullptr, 0);
+    return x ? x : dflt;
+}
+
+int run(Job &j, uint32_t n)
+{
+    if (n == 0) return HC_OK;
+    if (!j.in || !j.in_lens || !j.out || !j.out_caps || !j.out_lens || !j.status) return HC_ERR_ARG;
+    for (uint32_t i = 0; i < n; ++i)
+        if ((!j.in[i] && j.in_lens[i]) || (!j.out[i] && j.out_caps[i])) return HC_ERR_ARG;
+    if (!hc_device_ok()) return HC_ERR_DEVICE;
+    // sub-batch limits: input bytes and streams per slot (HC_PIPE_BYTES / HC_PIPE_STREAMS)
+    const uint64_t max_bytes = env_u64("HC_PIPE_BYTES", 1ull << 30);
+    const uint64_t max_streams = env_u64("HC_PIPE_STREAMS", 8192);
+    j.dcap.resize(n);
+    for (uint32_t i = 0; i < n; ++i) j.dcap[i] = guess_cap(j, i);
+    Slot slots[2];
+    for (Slot &s : slots) {
+        PIPE_CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+        PIPE_CK(hipEventCreateWithFlags(&s.meta_done, hipEventDisableTiming));
+    }
+    std::vector<uint32_t> order(n), redo;
+    for (uint32_t i = 0; i < n; ++i) order[i] = i;
+    for (int pass = 0; pass < 2 && !order.empty(); ++pass) {
+        // pass 1 codes the streams whose capacity guess fell short, one per sub-batch entry
+        std::vector<uint32_t> cur;
+        cur.swap(order);
+        uint32_t pos = 0, turn = 0;
+        while (pos < cur.size()) {
+            Slot &s = slots[turn++ & 1];
+            if (s.busy) {
+                const int rc = finish(j, s, redo);
+                if (rc) return rc;
+            }
+            // streams of one sub-batch must be contiguous in the job: pass 0 is in order; in
+            // pass 1 each stream forms its own sub-batch
+            uint64_t bytes = 0;
+            uint32_t cnt = 0;
+            if (pass == 0) {
+                while (pos + cnt < cur.size() && cnt < max_streams &&
+                       (cnt == 0 || bytes + j.in_lens[cur[pos + cnt]] <= max_bytes)) {
+                    bytes += j.in_lens[cur[pos + cnt]];
+                    ++cnt;
+                }
+            } else {
+                cnt = 1;
+            }
+            s.first = cur[pos];
+            s.count = cnt;
+            pos += cnt;
+            const int rc = launch(j, s);
+            if (rc) return rc;
+        }
+        for (int k = 0; k < 2; ++k) {
+            Slot &s = slots[turn++ & 1];
+            if (s.busy) {
+                const int rc = finish(j, s, redo);
+                if (rc) return rc;
+            }
+        }
+        order.swap(redo);
+        redo.clear();
+    }
+    return HC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hc_compress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, uint32_t n_streams,
+                           uint32_t flags, uint8_t *const *out, const uint64_t *out_caps,
+                           uint64_t *out_lens, int32_t *status)
+{
+    if (flags & ~HC_FLAG_DIFF) return HC_ERR_ARG;
+    Job j{true, flags, in, in_lens, out, out_caps, out_lens, status, {}};
+    return run(j, n_streams);
+}
+
+int hc_decompress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, uint32_t n_streams,
+                             uint8_t *const *out, const uint64_t *out_caps, uint64_t *out_lens,
+                             int32_t *status)
+{
+    Job j{false, 0, in, in_lens, out, out_caps, out_lens, status, {}};
+    return run(j, n_streams);
+}
+
+}  // extern "C"

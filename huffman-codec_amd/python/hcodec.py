@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 LIB_PATH = os.path.join(PKG, "lib", "libhcodec.so")
 CLI_PATH = os.path.join(PKG, "bin", "huffman-codec")
+BATCH_CLI_PATH = os.path.join(PKG, "bin", "huffman-codec-batch")
 INCLUDE_DIR = os.path.join(os.path.dirname(PKG), "include")
 
 HC_OK = 0
@@ -77,6 +78,8 @@ def lib():
     L.hc_compress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
                                     vp, vp]
     L.hc_decompress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
+    L.hc_compress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp]
+    L.hc_decompress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, vp, vp, vp, vp]
     L.hc_version.restype = ctypes.c_char_p
     L.hc_device_ok.restype = ctypes.c_int
     L.hc_device_info.argtypes = [ctypes.c_char_p, u64]
@@ -147,6 +150,38 @@ def decompress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, s
                                    _stream_handle(stream))
     if rc:
         raise HCodecError(f"hc_decompress_batch failed: {rc}")
+
+
+def _host_batch(fn, blobs, caps, *extra):
+    """blobs in host memory -> (statuses, outputs) through a host-batch entry point"""
+    n = len(blobs)
+    keep = [bytes(b) for b in blobs]
+    ins = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) if b else None
+                                          for b in keep])
+    lens = (ctypes.c_uint64 * max(n, 1))(*[len(b) for b in keep])
+    outs_buf = [ctypes.create_string_buffer(max(int(c), 1)) for c in caps]
+    outs = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(o, ctypes.c_void_p) for o in outs_buf])
+    ocaps = (ctypes.c_uint64 * max(n, 1))(*[int(c) for c in caps])
+    olens = (ctypes.c_uint64 * max(n, 1))()
+    st = (ctypes.c_int32 * max(n, 1))()
+    rc = fn(ctypes.cast(ins, ctypes.c_void_p), ctypes.cast(lens, ctypes.c_void_p), n, *extra,
+            ctypes.cast(outs, ctypes.c_void_p), ctypes.cast(ocaps, ctypes.c_void_p),
+            ctypes.cast(olens, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p))
+    if rc:
+        raise HCodecError(f"host batch failed: {rc}")
+    res = [outs_buf[i].raw[:olens[i]] if st[i] == 0 else b"" for i in range(n)]
+    return [st[i] for i in range(n)], res, [olens[i] for i in range(n)]
+
+
+def compress_host_batch(blobs, use_diff=False, caps=None):
+    """hc_compress_host_batch on host byte strings: (statuses, encoded, out_lens)."""
+    caps = caps if caps is not None else [compress_bound(len(b)) for b in blobs]
+    return _host_batch(lib().hc_compress_host_batch, blobs, caps, HC_FLAG_DIFF if use_diff else 0)
+
+
+def decompress_host_batch(blobs, caps):
+    """hc_decompress_host_batch on host byte strings: (statuses, decoded, out_lens)."""
+    return _host_batch(lib().hc_decompress_host_batch, blobs, caps)
 
 
 def synth_batch(kind, k0, n_streams, width, height, out, stride, stream=None):

@@ -97,6 +97,30 @@ int hc_decompress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64
                         const uint64_t *out_caps, uint64_t *out_lens, int32_t *status,
                         void *stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Host-buffer batch API — many independent streams in HOST memory (e.g. files read by the
+ * caller), synchronous. Beyond the reference, which codes one file per process
+ * (main.cpp:202-220); SURVEY.md §8f-1. The library stages the streams through pinned memory
+ * in sub-batches and overlaps each sub-batch's copies and kernels with the next one's (two
+ * HIP streams); only produced bytes cross PCIe. Stream i reads in[i][0 .. in_lens[i]) and
+ * writes out[i][0 .. out_caps[i]); out_lens[i] / status[i] as in the device batch API
+ * (HC_ERR_CAPACITY: out_lens[i] = bytes needed, nothing written). Sub-batch size: the
+ * environment variables HC_PIPE_BYTES (input bytes, default 1 GiB) and HC_PIPE_STREAMS
+ * (default 8192). The return value reports argument / device errors only.
+ * ------------------------------------------------------------------------------------- */
+
+/* flags: 0 or HC_FLAG_DIFF (adaptive streams go through hc_compress). out_caps[i] >=
+ * hc_compress_bound(in_lens[i], 0) always suffices. */
+int hc_compress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, uint32_t n_streams,
+                           uint32_t flags, uint8_t *const *out, const uint64_t *out_caps,
+                           uint64_t *out_lens, int32_t *status);
+
+/* Non-adaptive streams (flags bit 6 clear; others get HC_ERR_UNSUPPORTED: use
+ * hc_decompress). */
+int hc_decompress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, uint32_t n_streams,
+                             uint8_t *const *out, const uint64_t *out_caps, uint64_t *out_lens,
+                             int32_t *status);
+
 /* Library version string and a device check (1 = a gfx950 device is usable). */
 const char *hc_version(void);
 int hc_device_ok(void);

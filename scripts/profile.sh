@@ -26,6 +26,7 @@ for p in $PASSES; do
     inst) run pmc_inst 600 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE ;;
     wait) run pmc_wait 600 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_LDS_BANK_CONFLICT ;;
     branch) run pmc_branch 600 --kernel-trace --pmc SQ_INSTS_BRANCH SQ_INSTS_SENDMSG SQ_INSTS_VMEM SQ_INSTS_FLAT GRBM_GUI_ACTIVE ;;
+    occ) run pmc_occ 600 --kernel-trace --pmc SQ_LEVEL_WAVES SQ_WAVES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES ;;
     fetch) run pmc_fetch 600 --kernel-trace --pmc FETCH_SIZE ;;
     write) run pmc_write 600 --kernel-trace --pmc WRITE_SIZE ;;
     esac
