@@ -55,12 +55,14 @@ __device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t l
 
 // The issue arbiter prefers higher priority, then older waves: left alone, the oldest of a
 // SIMD's 8 waves run ahead and the last ones finish long after, on a half-empty SIMD. Waves
-// that are behind (by the quarter of their stream done) take a higher priority instead.
+// that are behind (by the share of their stream done: below 1/2, 4/5, 19/20, the rest) take a
+// higher priority instead. Within a band the arbiter goes by age, so the last bands are short.
 __device__ __forceinline__ void prio_by_progress(uint32_t done, uint32_t total)
 {
-    if ((uint64_t)done * 4 < total) __builtin_amdgcn_s_setprio(3);
-    else if ((uint64_t)done * 2 < total) __builtin_amdgcn_s_setprio(2);
-    else if ((uint64_t)done * 4 < 3ull * total) __builtin_amdgcn_s_setprio(1);
+    const uint64_t d = (uint64_t)done * 20;
+    if (d < 10ull * total) __builtin_amdgcn_s_setprio(3);
+    else if (d < 16ull * total) __builtin_amdgcn_s_setprio(2);
+    else if (d < 19ull * total) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 }
 
