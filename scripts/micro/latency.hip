@@ -77,14 +77,14 @@ __global__ __launch_bounds__(NT) void chain(uint64_t *out, int iters, uint64_t *
             (t1 - t0) + ((v + a1 + a2 + a3 + a4 + s + b1 + b2 + b3) & 1);
 }
 
-template <int T>
+template <int T, int LDSW = 4096>
 double run(int blocks, int iters)
 {
     uint64_t *d;
     const int waves = blocks * 4;
     hipMalloc(&d, waves * sizeof(uint64_t));
-    chain<T><<<blocks, 256>>>(d, iters, nullptr);  // warm
-    chain<T><<<blocks, 256>>>(d, iters, nullptr);
+    chain<T, LDSW><<<blocks, 256>>>(d, iters, nullptr);  // warm
+    chain<T, LDSW><<<blocks, 256>>>(d, iters, nullptr);
     hipDeviceSynchronize();
     uint64_t *h = new uint64_t[waves];
     hipMemcpy(h, d, waves * sizeof(uint64_t), hipMemcpyDeviceToHost);
@@ -171,5 +171,16 @@ int main()
     if (getenv("LAT_CHAINS")) {
         RUN(0) RUN(1) RUN(2) RUN(9) RUN(7) RUN(4) RUN(3) RUN(6) RUN(5) RUN(10) RUN(11) RUN(12) RUN(13)
     }
+    // issue throughput with full residency (no LDS: 8 waves per SIMD, checked above): per wave
+    // cycles per step of 4 independent instructions -> instructions per cycle per SIMD / CU
+    printf("throughput at 8 waves/SIMD (LDS-free kernels):\n");
+#define THRU(T, what)                                                                                \
+    {                                                                                                \
+        const double c1 = run<T, 16>(1, 2000), c8 = run<T, 16>(cus * 8, 2000);                      \
+        printf("  %-28s 1 wave/SIMD: %5.1f cyc/step; 8 waves/SIMD: %5.1f cyc/step = %.2f/cycle/SIMD, %.2f/cycle/CU\n", \
+               what, c1, c8, 8 * 4 / c8, 32 * 4 / c8);                                               \
+        fflush(stdout);                                                                              \
+    }
+    THRU(10, "4 indep VALU") THRU(11, "4 indep SALU") THRU(12, "2 VALU + 2 SALU")
     return 0;
 }
