@@ -378,6 +378,20 @@ struct Fgk {
         }
     }
 
+    // decoder: the position of symbol sym's leaf, 0xFFFFFFFF if it has none (lane-parallel scan
+    // of body[]; only a corrupted stream names a known symbol after the NYT code)
+    __device__ uint32_t find_leaf(uint32_t sym)
+    {
+        for (uint32_t r = 0; r * 64 <= kRoot; ++r) {
+            const uint32_t p = r * 64 + lane;
+            const uint32_t b = T.body[min(p, kRoot)];
+            // positions at or below the NYT are unused (body 0 would read as symbol 0)
+            const uint64_t m = ballot(p > nyt && p <= kRoot && !(b & (kInner | kNyt)) && (b & 255u) == sym);
+            if (m) return r * 64 + (uint32_t)__builtin_ctzll(m);
+        }
+        return 0xFFFFFFFFu;
+    }
+
     __device__ __forceinline__ uint32_t parent(uint32_t x) const
     {
         return kWide ? uni(T.up[x]) : (uni(T.wt[x]) & 1023u);
@@ -1082,9 +1096,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             }
             if (b & kNyt) {  // the new leaf below the NYT becomes level 0
                 sym = in.bits8();
-                x = uni(fgk.split(sym));
-                pv = __shfl_up(pv, 1, 64);
-                pv = lane == 0 ? x : pv;
+                // huffman.cpp:95-111 splits only for a symbol without a leaf; a corrupted stream
+                // can name a known one, whose own leaf is then updated
+                const uint32_t known = fgk.find_leaf(sym);
+                if (known == 0xFFFFFFFFu) {
+                    x = uni(fgk.split(sym));
+                    pv = __shfl_up(pv, 1, 64);
+                    pv = lane == 0 ? x : pv;
+                } else {
+                    fgk.chase(known, pv);
+                }
             }
             if (!(b & kInner)) fgk.update_path(pv);
             sbuf[i - 1 - i0] = (uint8_t)sym;

@@ -172,7 +172,7 @@ def ref_available(o2=False):
     return os.path.exists(REF_BIN_O2 if o2 else REF_BIN)
 
 
-def run_ref(args, input_bytes, workdir, o2=False):
+def run_ref(args, input_bytes, workdir, o2=False, timeout=None):
     """Run the compiled reference (oracle/_ref) on input_bytes. Returns (rc, output bytes, stderr)."""
     inp = os.path.join(workdir, "ref_in.bin")
     outp = os.path.join(workdir, "ref_out.bin")
@@ -181,7 +181,7 @@ def run_ref(args, input_bytes, workdir, o2=False):
     if os.path.exists(outp):
         os.remove(outp)
     r = subprocess.run([REF_BIN_O2 if o2 else REF_BIN] + list(args) + ["-i", inp, "-o", outp],
-                       capture_output=True)
+                       capture_output=True, timeout=timeout)
     out = b""
     if os.path.exists(outp):
         with open(outp, "rb") as f:
