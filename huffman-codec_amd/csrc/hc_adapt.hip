@@ -10,9 +10,10 @@
 // runs whose closed-form MNP-5 cost, SURVEY.md Appendix A.3, gives the block's RLE length
 // without emitting it); per-block min/argmin and the candidate's total follow; the host picks
 // the first minimum; an exclusive scan of the chosen lengths places each block; one lane per
-// block then emits its RLE bytes. Decode: one serial lane finds each block's start in the
-// symbol stream (the FSM cannot be split without knowing where blocks begin), then one lane
-// per block reverts and scatters in parallel; the diff revert is a parallel mod-256 scan.
+// block then emits its RLE bytes. Decode: one wavefront finds each block's start in the symbol
+// stream (a wave scan of the revert machine's transition functions and of output lengths per
+// 256 symbols), then one lane per block reverts and scatters in parallel; the diff revert is a
+// parallel mod-256 scan.
 #include <hipcub/hipcub.hpp>
 
 #include <vector>
@@ -253,45 +254,128 @@ __global__ void emit_kernel(const uint8_t *m, uint64_t w, uint64_t h, uint64_t b
 
 // ------------------------------------------------------------------------------ decode ---
 
-// One lane: find where each block's RLE data starts (transform.cpp:162-187 run block by
-// block), reporting 13 / 14 / 15 exactly where the reference would exit.
-__global__ void bounds_kernel(const uint8_t *sym, uint64_t nsym, uint64_t w, uint64_t h,
-                              uint64_t b, uint64_t nb, uint64_t pos0, uint64_t *start,
-                              int *status)
+// Where each block's RLE data starts (transform.cpp:330-361 running revertRLEBlock,
+// transform.cpp:162-187, block by block), reporting 13 / 14 / 15 exactly where the reference
+// exits. One wavefront, 256 symbols per step (4 per lane). The revert machine's state r (0..3:
+// how many equal literals precede; 3 = the next symbol is a count) moves by one of two functions
+// per symbol — a literal repeating the previous symbol (r -> r + 1) or not (r -> 1), a count -> 0;
+// from 0 both give 1, so the symbol before a block start never matters. A wave scan of their
+// compositions gives each symbol's state, hence its output length (count: the symbol, literal:
+// 1); a scan of lengths finds the first symbol where the block's byte count is reached. A block
+// that ends inside the step re-scans the rest of the same registers from state 0.
+constexpr uint32_t kFsmEq = 1u | 2u << 2 | 3u << 4;        // r: 0->1 1->2 2->3 3->0
+constexpr uint32_t kFsmNe = 1u | 1u << 2 | 1u << 4;        // r: 0->1 1->1 2->1 3->0
+constexpr uint32_t kFsmId = 0u | 1u << 2 | 2u << 4 | 3u << 6;
+
+__device__ __forceinline__ uint32_t fsm_then(uint32_t g, uint32_t f)  // x -> g(f(x))
 {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint64_t pos = pos0;
-    for (uint64_t i = 0; i < nb; ++i) {
-        const Geo g = block_geo(w, h, b, i);
-        const uint64_t want = g.sx * g.sy;
-        start[i] = pos;
-        uint64_t got = 0;
-        uint32_t run_byte = 0, run = 0;
-        while (got < want) {
-            if (pos >= nsym) {
-                *status = HC_ERR_BLOCK_EOF;
-                return;
-            }
-            const uint32_t c = sym[pos++];
-            if (run == 3) {
-                got += c;
-                run = 0;
-            } else {
-                ++got;
-                if (c == run_byte) ++run;
-                else {
-                    run_byte = c;
-                    run = 1;
-                }
-            }
-        }
-        if (got != want) {
-            *status = HC_ERR_BLOCK_DATA;
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < 4; ++x) h |= ((g >> (2 * ((f >> (2 * x)) & 3u))) & 3u) << (2 * x);
+    return h;
+}
+
+__global__ __launch_bounds__(64) void bounds_kernel(const uint8_t *sym, uint64_t nsym, uint64_t w,
+                                                    uint64_t h, uint64_t b, uint64_t nb, uint64_t pos0,
+                                                    uint64_t *start, int *status)
+{
+    const uint32_t lane = threadIdx.x;
+    uint64_t pos = pos0;  // first symbol of the loaded step
+    uint64_t blk = 0, got = 0;
+    uint32_t r = 0, last = 0;  // machine state and previous symbol at the step's start
+    if (lane == 0) start[0] = pos;
+    uint64_t want = 0;
+    if (nb) {
+        const Geo g = block_geo(w, h, b, 0);
+        want = g.sx * g.sy;
+    }
+    while (blk < nb) {
+        const uint64_t avail = nsym - pos;
+        const uint32_t m = avail < 256 ? (uint32_t)avail : 256u;
+        if (m == 0) {  // transform.cpp:170-174: the block wants more, the stream is empty
+            if (lane == 0) *status = HC_ERR_BLOCK_EOF;
             return;
         }
+        uint32_t x[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) x[k] = 4 * lane + k < m ? sym[pos + 4 * lane + k] : 0u;
+        const uint32_t up = __shfl_up(x[3], 1, 64);
+        uint32_t lo = 0;  // symbols below lo belong to blocks already closed
+        for (;;) {
+            uint32_t f[4], F = kFsmId;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t i = 4 * lane + k;
+                const uint32_t p = k ? x[k - 1] : (lane ? up : last);
+                f[k] = (i >= lo && i < m) ? (x[k] == p ? kFsmEq : kFsmNe) : kFsmId;
+                F = fsm_then(f[k], F);
+            }
+            uint32_t inc = F;
+            for (uint32_t off = 1; off < 64; off <<= 1) {
+                const uint32_t g = __shfl_up(inc, off, 64);
+                inc = lane >= off ? fsm_then(inc, g) : inc;
+            }
+            const uint32_t ex = __shfl_up(inc, 1, 64);
+            uint32_t s = ((lane ? ex : kFsmId) >> (2 * r)) & 3u;
+            uint32_t len[4], tot = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t i = 4 * lane + k;
+                len[k] = (i >= lo && i < m) ? (s == 3 ? x[k] : 1u) : 0u;
+                tot += len[k];
+                s = (f[k] >> (2 * s)) & 3u;
+            }
+            uint32_t acc = tot;  // inclusive scan of lengths (<= 256 * 255)
+            for (uint32_t off = 1; off < 64; off <<= 1) {
+                const uint32_t g = __shfl_up(acc, off, 64);
+                acc += lane >= off ? g : 0u;
+            }
+            const uint64_t need = want - got;  // >= 1
+            const uint64_t hit = __ballot((uint64_t)acc >= need);
+            if (!hit) {  // the block goes on past this step
+                got += __shfl(acc, 63, 64);
+                r = (__shfl(inc, 63, 64) >> (2 * r)) & 3u;
+                const uint32_t lt = __shfl(x[(m - 1) & 3u], (m - 1) >> 2, 64);
+                last = lt;
+                pos += m;
+                break;
+            }
+            // the first symbol whose running length reaches the block's size closes it
+            const uint32_t L = (uint32_t)__builtin_ctzll(hit);
+            uint32_t c = acc - tot, j = 0xFFFFFFFFu, cj = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                c += len[k];
+                if (j == 0xFFFFFFFFu && (uint64_t)c >= need) {
+                    j = 4 * lane + k;
+                    cj = c;
+                }
+            }
+            j = __shfl(j, L, 64);
+            cj = __shfl(cj, L, 64);
+            if ((uint64_t)cj != need) {  // transform.cpp:178-182: a count overshoots the block
+                if (lane == 0) *status = HC_ERR_BLOCK_DATA;
+                return;
+            }
+            lo = j + 1;
+            ++blk;
+            if (lane == 0) start[blk] = pos + lo;
+            if (blk == nb) {
+                pos += lo;
+                break;
+            }
+            const Geo g = block_geo(w, h, b, blk);
+            want = g.sx * g.sy;
+            got = 0;
+            r = 0;
+            if (lo == m) {
+                pos += m;
+                break;
+            }
+        }
     }
-    *status = pos != nsym ? HC_ERR_LEFTOVER : 0;
-    start[nb] = pos;
+    // transform.cpp:354-358
+    if (lane == 0) *status = pos != nsym ? HC_ERR_LEFTOVER : 0;
 }
 
 // transform.cpp:162-216 for one block per lane: revert its RLE and scatter in scan order

@@ -65,14 +65,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--skip-c4", action="store_true")
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5", help="comma-separated subset of C1..C5")
     args = ap.parse_args()
+    only = set(args.only.upper().split(","))
+    if args.skip_c4:
+        only.discard("C4")
     import torch
     import hcodec as hc
     import oracle
     res = {"device": hc.device_info()}
 
     # C1: the reference binary on hd01 (rebuilt from the committed reference output)
-    if oracle.ref_available():
+    if "C1" in only and oracle.ref_available():
         with tempfile.TemporaryDirectory() as d:
             huf = os.path.join(ROOT, "tests", "golden", "corpus", "hd01.cm.huf")
             subprocess.run([oracle.REF_BIN, "-d", "-i", huf, "-o", os.path.join(d, "hd01.raw")], check=True,
@@ -90,21 +94,23 @@ def main():
     print(json.dumps({"C1": res.get("C1")}), flush=True)
 
     # C2: one stream (a lone wavefront)
-    (te, td), ok, nbytes, first, raw0 = batch_round_trip(hc, torch, 1, "photo", True, reps=5)
-    res["C2"] = {"what": "1 x 512x512 photo -c -m, one wavefront", "encode_ms": round(te, 3),
-                 "decode_ms": round(td, 3), "bytes": nbytes, "round_trip_exact": ok,
-                 "oracle_identical": first == oracle.compress(raw0, True, False, 512)[1]}
-    print(json.dumps({"C2": res["C2"]}), flush=True)
+    if "C2" in only:
+        (te, td), ok, nbytes, first, raw0 = batch_round_trip(hc, torch, 1, "photo", True, reps=5)
+        res["C2"] = {"what": "1 x 512x512 photo -c -m, one wavefront", "encode_ms": round(te, 3),
+                     "decode_ms": round(td, 3), "bytes": nbytes, "round_trip_exact": ok,
+                     "oracle_identical": first == oracle.compress(raw0, True, False, 512)[1]}
+        print(json.dumps({"C2": res["C2"]}), flush=True)
 
     # C3: 4096 streams -c
-    (te, td), ok, nbytes, first, raw0 = batch_round_trip(hc, torch, 4096, "photo", False)
-    res["C3"] = {"what": "4096 x 512x512 photo -c", "encode_ms": round(te, 3), "decode_ms": round(td, 3),
-                 "GiBps_enc_dec": round(4096 * N / ((te + td) * 1e-3) / 2**30, 4), "bytes": nbytes,
-                 "round_trip_exact": ok, "stream0_oracle_identical": first == oracle.compress(raw0, False, False, 512)[1]}
-    print(json.dumps({"C3": res["C3"]}), flush=True)
+    if "C3" in only:
+        (te, td), ok, nbytes, first, raw0 = batch_round_trip(hc, torch, 4096, "photo", False)
+        res["C3"] = {"what": "4096 x 512x512 photo -c", "encode_ms": round(te, 3), "decode_ms": round(td, 3),
+                     "GiBps_enc_dec": round(4096 * N / ((te + td) * 1e-3) / 2**30, 4), "bytes": nbytes,
+                     "round_trip_exact": ok, "stream0_oracle_identical": first == oracle.compress(raw0, False, False, 512)[1]}
+        print(json.dumps({"C3": res["C3"]}), flush=True)
 
     # C4: one 4096x4096 matrix, adaptive block RLE, single-buffer API (host buffers)
-    if not args.skip_c4:
+    if "C4" in only:
         buf = torch.empty(4096 * 4096, dtype=torch.uint8, device="cuda")
         hc.synth_batch("photo", 0, 1, 4096, 4096, buf, 0)
         raw = buf.cpu().numpy().tobytes()
@@ -121,11 +127,12 @@ def main():
             print(json.dumps({"C4" + ("m" if use_diff else ""): res["C4" + ("m" if use_diff else "")]}), flush=True)
 
     # C5: the per-GPU shard (bench.py's workload)
-    (te, td), ok, nbytes, _, _ = batch_round_trip(hc, torch, 8192, "photo", True)
-    res["C5"] = {"what": "8192 x 512x512 photo -c -m round trip (per-GPU shard of 65536)", "encode_ms": round(te, 3),
-                 "decode_ms": round(td, 3), "GiBps_enc_dec": round(8192 * N / ((te + td) * 1e-3) / 2**30, 4),
-                 "bytes": nbytes, "round_trip_exact": ok}
-    print(json.dumps({"C5": res["C5"]}), flush=True)
+    if "C5" in only:
+        (te, td), ok, nbytes, _, _ = batch_round_trip(hc, torch, 8192, "photo", True)
+        res["C5"] = {"what": "8192 x 512x512 photo -c -m round trip (per-GPU shard of 65536)", "encode_ms": round(te, 3),
+                     "decode_ms": round(td, 3), "GiBps_enc_dec": round(8192 * N / ((te + td) * 1e-3) / 2**30, 4),
+                     "bytes": nbytes, "round_trip_exact": ok}
+        print(json.dumps({"C5": res["C5"]}), flush=True)
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
