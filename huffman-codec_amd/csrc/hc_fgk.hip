@@ -120,6 +120,13 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x)
 {
     return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
 }
+// the value unchanged, opaque to the optimizer: a u16 LDS load kept as a 32-bit value (left
+// alone, masks of it are narrowed to 16-bit ops that cost an extra re-extension each)
+__device__ __forceinline__ uint32_t opaque(uint32_t x)
+{
+    asm("" : "+v"(x));
+    return x;
+}
 __device__ __forceinline__ uint32_t lane_id()
 {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -1045,26 +1052,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             const uint32_t lane8 = min(lane + 8, 31u);  // lane k: shift for level d - k
             uint32_t e8 = uni(fgk.T.lvl[(uint32_t)(in.win >> 56) + 254]);
             uint32_t v, d, x, b, pv, k;
+            // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
+            // both sign bits set, one scalar AND
+            int32_t left = (int32_t)(i - i1);
+            uint32_t so = vreg(i - i0);  // the symbol's byte in sbuf (a VGPR: no scalar copy per symbol)
             do {
                 v = (uint32_t)(in.win >> 56);
                 x = e8 & 1023u;
                 d = e8 >> 10;
-                b = fgk.T.body[x];
+                b = opaque(fgk.T.body[x]);
                 // level j's entry for prefix v >> (8 - j) sits at ((256 | v) >> (8 - j)) - 2;
                 // lane k needs j = d - k; lanes k >= d shift by >= 8 and read lvl_root
-                const uint32_t pr = fgk.T.lvl[((256u | v) >> (lane8 - d)) - 2];
+                const uint32_t pr = opaque(fgk.T.lvl[((256u | v) >> (lane8 - d)) - 2]);
                 in.win <<= d;
                 in.nwin -= d;  // >= 25
-                const uint32_t e8n = fgk.T.lvl[(uint32_t)(in.win >> 56) + 254];  // next symbol
+                const uint32_t e8n = opaque(fgk.T.lvl[(uint32_t)(in.win >> 56) + 254]);  // next symbol
                 pv = pr & 1023u;
                 // a leaf's body is its symbol; inner / NYT (bits 8, 9): force the failure
                 const uint32_t force = 0u - __builtin_amdgcn_ubfe(b, 8, 2);
                 k = fgk.update_fast(pv, [] {}, force);
-                sbuf[i - i0] = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
-                ++i;
+                sbuf[so] = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
+                so = so + 1;
+                ++left;
                 if (in.nwin <= 32) in.refill();
                 e8 = uni(e8n);
-            } while (k == 0xFFFFFFFFu && i < i1);
+            } while ((int32_t)(k & (uint32_t)left) < 0);
+            i = i0 + uni(so);
             if (k == 0xFFFFFFFFu) continue;
             // symbol i - 1 left the loop: the window stands d bits into its code
             b = uni(b);
