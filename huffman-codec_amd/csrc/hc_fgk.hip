@@ -114,6 +114,7 @@ struct alignas(16) Tree {
 };
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;  // a byte in LDS (32-bit address)
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x)
@@ -762,27 +763,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
             uint32_t e0 = ws0 >> 10;
             uint32_t pr0 = vreg(fgk.pc_lane[e0 * kRow]);   // cache row of t (pc_miss if none)
             uint32_t sv2 = vreg(sb[vt + 2]);               // byte of t+2
-            uint32_t e, pv, k;
+            // LDS address of the byte of t+3, in a VGPR (one add per symbol, no base add)
+            const lds_u8 *vb = (const lds_u8 *)sb + t + 3;
+            asm("" : "+v"(vb));
+            uint32_t pv, k;
+            // loop while no level failed (k = 0xFFFFFFFF) and record lanes are left (left < 0):
+            // both sign bits set, one scalar AND
+            int32_t left = (int32_t)(rl - rend);
             do {
-                e = e0;
-                const uint32_t rec = fgk.pc_use(e, pr0, pv);
+                const uint32_t rec = fgk.pc_use(e0, pr0, pv);
                 k = fgk.update_fast(pv, [&] {
-                    const uint32_t e1 = ws1 >> 10;
-                    const uint32_t pr1 = fgk.pc_lane[e1 * kRow];
+                    // (v_bfe + v_lshl_add; left alone the compiler emits shift, and, add)
+                    const uint32_t pr1 = fgk.pc_lane[opaque(__builtin_amdgcn_ubfe(ws1, 10, 6)) * kRow];
                     const uint32_t ws2 = fgk.T.where[sv2];
-                    const uint32_t sv3 = sb[vt + 3];
-                    e0 = e1;
+                    const uint32_t sv3 = *vb;
                     pr0 = pr1;
                     ws1 = ws2;
                     sv2 = sv3;
                 });
-                sink.vrec = writelane(sink.vrec, rec, rl);
-                vt = vreg(vt + 1);
-                ++rl;
-            } while (k == 0xFFFFFFFFu && rl < rend);
+                sink.vrec = writelane(sink.vrec, rec, (uint32_t)((int32_t)rend + left));
+                ++vb;
+                ++left;
+            } while ((int32_t)(k & (uint32_t)left) < 0);
+            rl = (uint32_t)((int32_t)rend + left);
             t += rl - sink.n;
             if (k != 0xFFFFFFFFu) {
-                if (any(e == 0)) {  // not cached: nothing was written; code it from scratch
+                // not cached (the miss row's sentinel at level 0): nothing was written; code it
+                // from scratch
+                if (lane_read(pv, 0) == kMissPos) {
                     --t;
                     sink.n = rl - 1;  // its record lane, overwritten by the miss path
                     miss(sb[t]);
