@@ -478,6 +478,8 @@ struct Fgk {
         ahead();  // the caller's reads for later symbols go out behind these
         const uint64_t fail = ballot(w1 <= (kWide ? (w0 | force | (force >> 1)) : (w0 | 1023u | force)));
         const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
+        // (measured: an exec-masked store, s_bfm + save/restore of exec instead of this compare
+        // and select, made the encoder 3 % slower)
         *(lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
         __builtin_amdgcn_wave_barrier();
         return k;
