@@ -407,20 +407,28 @@ struct Fgk {
 
     // Encoder: the path from position s to the root, BEFORE the update (the code of
     // huffman.cpp:136-155): the position of level k (0 = s) goes to lane k; returns the levels.
+    // Each level enters at lane 0 by a DPP wave shift (lane 0 keeps the new position), so the
+    // path arrives top-down; one permute turns it bottom-up at the end.
     __device__ __forceinline__ uint32_t chase(uint32_t s0, uint32_t &pv)
     {
-        uint32_t k = 0;
+        int32_t km = -64;       // levels - 64
         uint32_t s = vreg(s0);  // per-level work on the VALU (see vreg)
-        pv = kRoot;
-        for (;;) {
-            pv = lane == k ? s : pv;
-            ++k;
-            const uint32_t p = kWide ? (uint32_t)T.up[s] : (T.wt[s] & 1023u);
-            s = max(p, s + 1);  // parents sit above children; max() bounds a bug
-            if (!ballot(s < kRoot)) break;
-        }
+        uint32_t td = kRoot;    // lane j: level k - 1 - j
+        do {
+            // wave_shr:1, lane 0 taking s
+            const uint32_t sh = __builtin_amdgcn_update_dpp(0u, td, 0x138, 0xF, 0xF, true);
+            td = lane == 0 ? s : sh;
+            ++km;
+            s = kWide ? (uint32_t)T.up[s] : (T.wt[s] & 1023u);
+            // go on while s is not the root (x - 1 >= 0) and fewer than 64 levels (km < 0;
+            // parents sit above children, so this only bounds a bug): one sign test
+        } while ((int32_t)((uint32_t)km & ~((uni(s) ^ kRoot) - 1u)) < 0);
+        uint32_t k = (uint32_t)(km + 64);
+        asm volatile("" : "+s"(k));  // the depth, opaque: no loop-strength-reduced copies of it
         bad |= uni(s) ^ kRoot;
-        bad |= k > 64 ? 1u : 0u;
+        const uint32_t j = k - 1 - lane;  // lane < k: the lane holding this lane's level
+        pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((j & 63u) * 4), (int)td);
+        pv = lane < k ? pv : kRoot;
         return k;
     }
 
@@ -435,6 +443,9 @@ struct Fgk {
             uint32_t ws = uni(v);
             const uint64_t le = ballot(v <= (kWide ? ws : (ws | 1023u)));
             uint32_t p = kWide ? uni(T.up[s]) : (ws & 1023u);
+            // lane 0 read position s: its address and word, incremented, are the store's
+            uint32_t *dst = &T.wt[s + lane];
+            uint32_t nv = v + kInc;
             if ((uint32_t)le & 2u) {  // s+1 weighs the same: find the block leader
                 const uint32_t lead =
                     ~le ? s + (uint32_t)__builtin_ctzll(~le) - 1 : leader_far(s + 64, ws);
@@ -446,9 +457,11 @@ struct Fgk {
                     ws = off < 64 ? lane_read(v, off) : uni(T.wt[lead]);
                     s = lead;
                     p = kWide ? uni(T.up[s]) : (ws & 1023u);
+                    dst = &T.wt[s];
+                    nv = ws + kInc;
                 }
             }
-            *(lane == 0 ? &T.wt[s] : scr32()) = ws + kInc;
+            *(lane == 0 ? dst : scr32()) = nv;
             __builtin_amdgcn_wave_barrier();
             s = max(p, s + 1);
             if (s >= kRoot) break;
