@@ -10,7 +10,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libhcodec.so")
+# HC_LIB_PATH: another build of the same library (A/B timing of kernel variants in one run)
+LIB_PATH = os.environ.get("HC_LIB_PATH") or os.path.join(PKG, "lib", "libhcodec.so")
 CLI_PATH = os.path.join(PKG, "bin", "huffman-codec")
 BATCH_CLI_PATH = os.path.join(PKG, "bin", "huffman-codec-batch")
 INCLUDE_DIR = os.path.join(os.path.dirname(PKG), "include")
