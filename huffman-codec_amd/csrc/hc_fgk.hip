@@ -273,28 +273,26 @@ struct Fgk {
         pc_free |= 1u << e;
     }
 
-    // positions s and l traded contents: drop every cached path through either. Per read,
-    // lane k holds levels 2(k&7), 2(k&7)+1 of entry k>>3 (+8 in the second read); words 6..7 of
-    // a row are metadata. Byte e of a ballot flags an entry.
+    // positions s and l traded contents: drop every cached path through either. Read r covers
+    // entries 4r..4r+3, one position per lane (lane 16j + k: level k of entry 4r + j; words
+    // 12..15 of a row are metadata, masked out of the ballot); 16-bit segment j flags entry
+    // 4r + j.
     __device__ __forceinline__ void pc_swapped(uint32_t s, uint32_t l)
     {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(T.pc);
-        const uint32_t ss = s | (s << 16), ll = l | (l << 16);
-        auto hit = [&](uint32_t q) -> uint32_t {
-            const uint32_t a = q ^ ss, c = q ^ ll;
-            return (uint32_t)((lane & 7u) < kSlotDepth / 2) &
-                   (((a & 0xFFFFu) == 0) | ((a >> 16) == 0) | ((c & 0xFFFFu) == 0) | ((c >> 16) == 0));
-        };
-        uint64_t m0 = ballot(hit(w[lane])), m1 = ballot(hit(w[64 + lane]));
-        while (m0) {
-            const uint32_t e = (uint32_t)__builtin_ctzll(m0) >> 3;
-            m0 &= ~(0xFFull << (8 * e));
-            pc_drop(e);
-        }
-        while (m1) {
-            const uint32_t e = (uint32_t)__builtin_ctzll(m1) >> 3;
-            m1 &= ~(0xFFull << (8 * e));
-            pc_drop(e + 8);
+        constexpr uint64_t kLevels = 0x0FFF0FFF0FFF0FFFull;
+        uint32_t q[kSlots / 4];
+        uint64_t m[kSlots / 4];
+#pragma unroll
+        for (uint32_t r = 0; r < kSlots / 4; ++r) q[r] = T.pc[64 * r + lane];
+#pragma unroll
+        for (uint32_t r = 0; r < kSlots / 4; ++r) m[r] = (ballot(q[r] == s) | ballot(q[r] == l)) & kLevels;
+#pragma unroll
+        for (uint32_t r = 0; r < kSlots / 4; ++r) {
+            while (m[r]) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(m[r]) >> 4;
+                m[r] &= ~(0xFFFFull << (16 * j));
+                pc_drop(4 * r + j);
+            }
         }
     }
 
