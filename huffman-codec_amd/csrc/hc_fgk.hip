@@ -128,6 +128,14 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x)
     asm("" : "+v"(x));
     return x;
 }
+// bits 56..63 of a wave-uniform u64, computed on the vector unit (a VGPR): the address it
+// feeds is then one v_lshl_add, not three scalar ops and a copy
+__device__ __forceinline__ uint32_t top8(uint64_t w)
+{
+    uint32_t r;
+    asm("v_lshrrev_b32 %0, 24, %1" : "=v"(r) : "s"((uint32_t)(w >> 32)));
+    return r;
+}
 __device__ __forceinline__ uint32_t lane_id()
 {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -1071,15 +1079,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // (a longer code or a stale table: body inner; the NYT; a failed leader test) is
             // forced to fail at level 0 so nothing is stored, and is finished outside.
             const uint32_t lane8 = min(lane + 8, 31u);  // lane k: shift for level d - k
-            uint32_t e8 = uni(fgk.T.lvl[(uint32_t)(in.win >> 56) + 254]);
+            // the level-8 entry of the next code: e8v as read (the VGPR: the body address is
+            // computed on the vector unit), e8 its scalar copy (the depth, for the window)
+            uint32_t e8v = opaque(fgk.T.lvl[(uint32_t)(in.win >> 56) + 254]);
+            uint32_t e8 = uni(e8v);
             uint32_t v, d, x, b, pv, k;
             // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
             // both sign bits set, one scalar AND
             int32_t left = (int32_t)(i - i1);
-            uint32_t so = vreg(i - i0);  // the symbol's byte in sbuf (a VGPR: no scalar copy per symbol)
+            lds_u8 *so = (lds_u8 *)sbuf + (i - i0);  // the symbol's byte (LDS address in a VGPR)
+            asm("" : "+v"(so));
             do {
                 v = (uint32_t)(in.win >> 56);
-                x = e8 & 1023u;
+                x = e8v & 1023u;
                 d = e8 >> 10;
                 b = opaque(fgk.T.body[x]);
                 // level j's entry for prefix v >> (8 - j) sits at ((256 | v) >> (8 - j)) - 2;
@@ -1087,18 +1099,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                 const uint32_t pr = opaque(fgk.T.lvl[((256u | v) >> (lane8 - d)) - 2]);
                 in.win <<= d;
                 in.nwin -= d;  // >= 25
-                const uint32_t e8n = opaque(fgk.T.lvl[(uint32_t)(in.win >> 56) + 254]);  // next symbol
+                const uint32_t e8n = opaque(fgk.T.lvl[top8(in.win) + 254]);  // next symbol
                 pv = pr & 1023u;
                 // a leaf's body is its symbol; inner / NYT (bits 8, 9): force the failure
                 const uint32_t force = 0u - __builtin_amdgcn_ubfe(b, 8, 2);
                 k = fgk.update_fast(pv, [] {}, force);
-                sbuf[so] = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
-                so = so + 1;
+                *so++ = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
                 ++left;
                 if (in.nwin <= 32) in.refill();
+                e8v = e8n;
                 e8 = uni(e8n);
             } while ((int32_t)(k & (uint32_t)left) < 0);
-            i = i0 + uni(so);
+            i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
             if (k == 0xFFFFFFFFu) continue;
             // symbol i - 1 left the loop: the window stands d bits into its code
             b = uni(b);
