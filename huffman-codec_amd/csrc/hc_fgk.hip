@@ -1068,8 +1068,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
         uint32_t i = i0;
         while (i < i1) {
             // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
-            // where the walk from the root stops (depth d <= 8); lane k < d reads level d-k's
-            // entry for the same prefix, the position of path level k (0 = the leaf).
+            // where the walk from the root stops (depth d <= 8), the levels above give the
+            // positions the walk passes.
             if (fgk.stale >= kRefresh) fgk.build_levels();
             if (in.nwin <= 32) in.refill();
             // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
@@ -1078,37 +1078,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // loop, and the loop is re-entered after them). Anything else
             // (a longer code or a stale table: body inner; the NYT; a failed leader test) is
             // forced to fail at level 0 so nothing is stored, and is finished outside.
-            const uint32_t lane8 = min(lane + 8, 31u);  // lane k: shift for level d - k
-            // the level-8 entry of the next code: e8v as read (the VGPR: the body address is
-            // computed on the vector unit), e8 its scalar copy (the depth, for the window)
-            uint32_t e8v = opaque(fgk.T.lvl[(uint32_t)(in.win >> 56) + 254]);
-            uint32_t e8 = uni(e8v);
-            uint32_t v, d, x, b, pv, k;
+            // lane k reads level 8 - k's entry for the code's 8-bit prefix v, at
+            // ((256 | v) >> k) - 2: levels >= d repeat the leaf's entry (position | depth d), so
+            // lanes 0..8-d hold the leaf, lanes 9-d..7 its ancestors (level 8-k), lane 8 and up
+            // the root pad (lvl_root). One read gives the depth (lane 0) and the whole root path
+            // (duplicated lanes store the same word); it depends only on the window, so the next
+            // code's read goes out as soon as this code's depth is known.
+            const uint32_t vk = min(lane, 9u);
+            uint32_t pr = opaque(fgk.T.lvl[((256u | (uint32_t)(in.win >> 56)) >> vk) - 2]);
+            uint32_t d, x, b, pv, k;
             // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
             // both sign bits set, one scalar AND
             int32_t left = (int32_t)(i - i1);
             lds_u8 *so = (lds_u8 *)sbuf + (i - i0);  // the symbol's byte (LDS address in a VGPR)
             asm("" : "+v"(so));
             do {
-                v = (uint32_t)(in.win >> 56);
-                x = e8v & 1023u;
+                const uint32_t e8 = uni(pr);  // the leaf's entry
+                x = e8 & 1023u;
                 d = e8 >> 10;
                 b = opaque(fgk.T.body[x]);
-                // level j's entry for prefix v >> (8 - j) sits at ((256 | v) >> (8 - j)) - 2;
-                // lane k needs j = d - k; lanes k >= d shift by >= 8 and read lvl_root
-                const uint32_t pr = opaque(fgk.T.lvl[((256u | v) >> (lane8 - d)) - 2]);
+                pv = pr & 1023u;
                 in.win <<= d;
                 in.nwin -= d;  // >= 25
-                const uint32_t e8n = opaque(fgk.T.lvl[top8(in.win) + 254]);  // next symbol
-                pv = pr & 1023u;
+                const uint32_t prn = opaque(fgk.T.lvl[((256u | (uint32_t)(in.win >> 56)) >> vk) - 2]);
                 // a leaf's body is its symbol; inner / NYT (bits 8, 9): force the failure
                 const uint32_t force = 0u - __builtin_amdgcn_ubfe(b, 8, 2);
                 k = fgk.update_fast(pv, [] {}, force);
                 *so++ = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
                 ++left;
                 if (in.nwin <= 32) in.refill();
-                e8v = e8n;
-                e8 = uni(e8n);
+                pr = prn;
             } while ((int32_t)(k & (uint32_t)left) < 0);
             i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
             if (k == 0xFFFFFFFFu) continue;
@@ -1127,8 +1126,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                 uint32_t depth = uni(d);
                 x = uni(x);
                 fgk.stale += depth < 8 ? 1u : 0u;
-                const uint32_t jl = 64 - lane, jc = jl > 8 ? 8 : jl;
-                uint32_t pt = fgk.T.lvl[(1u << jc) - 2 + (uni(v) >> (8 - jc))] & 1023u;
+                // levels 1..8 of the prefix, lane 64 - j <- level j (lane 8 - j of the path read)
+                uint32_t pt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 56) & 63u) * 4), (int)pv);
                 do {
                     x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
                     pt = lane == 63 - depth ? x : pt;
