@@ -83,7 +83,9 @@ constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte ch
                                     // >= 3, so such bytes are >= 3 apart)
 constexpr uint32_t kRefresh = 16;   // decoder: rebuild the level tables after this many lookups
                                     // they left short of depth 8
-constexpr uint32_t kMarkShift = 10; // decoder: body bits 10..15 = table generation (per position)
+constexpr uint32_t kMarkShift = 10; // decoder: body bits 10..14 = table generation (per position)
+constexpr uint32_t kNotLeaf = 0x8000; // decoder: body bit 15 = inner or NYT (moves with the content)
+constexpr uint32_t kContent = 0x83FF; // decoder: the body bits that move with the content
 
 // One wavefront's LDS; <= 5 KB so that 8 four-wave workgroups fit a CU. Encoder and decoder
 // each add their cache (tests/fgk_cache_model.py is the executable model of both, checked
@@ -115,6 +117,18 @@ struct alignas(16) Tree {
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // a byte in LDS (32-bit address)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+// the 32-bit LDS address of a word of the wave's tree
+__device__ __forceinline__ uint32_t lds_off(uint32_t *p) { return (uint32_t)(size_t)(lds_u32 *)p; }
+__device__ __forceinline__ uint32_t lds_off16(uint16_t *p) { return (uint32_t)(size_t)(lds_u16 *)p; }
+// b + 2 a on the scalar unit, one instruction (wave-uniform operands)
+__device__ __forceinline__ uint32_t lshl1_add(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("s_lshl1_add_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
+    return r;
+}
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x)
@@ -155,7 +169,22 @@ __device__ __forceinline__ bool any(bool p) { return ballot(p) != 0; }
 __device__ __forceinline__ uint32_t ff1(uint64_t m)
 {
     uint32_t r;
-    asm volatile("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+    asm("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+    return r;
+}
+// the lanes below k: (1 << (k & 63)) - 1 (k = 0xFFFFFFFF: lanes 0..62; in every path vector lane
+// 63 holds the root, whose duplicates in the lanes below it store the same word)
+__device__ __forceinline__ uint64_t below_mask(uint32_t k)
+{
+    uint64_t r;
+    asm("s_bfm_b64 %0, %1, 0" : "=s"(r) : "s"(k));
+    return r;
+}
+// per lane: bit lane of m ? t : f (one v_cndmask on a scalar mask)
+__device__ __forceinline__ uint32_t sel(uint64_t m, uint32_t t, uint32_t f)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
     return r;
 }
 // A wave-uniform value held in a VGPR: hiding its uniformity from the compiler moves the
@@ -210,7 +239,7 @@ struct Fgk {
         for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
         if (lane < 2) T.lvl_root[lane] = kRoot;
         for (uint32_t i = lane; i < 516; i += 64) {
-            T.body[i] = i == kRoot ? kNyt : 0;
+            T.body[i] = i == kRoot ? (kDec ? kNyt | kNotLeaf : kNyt) : 0;
             if (kWide) T.up[i] = 0;
         }
         if (!kDec) {
@@ -310,7 +339,7 @@ struct Fgk {
     // moves the content of a position some walk passes through: those carry the generation.
     __device__ void build_levels()
     {
-        gen = gen == 63 ? 1u : gen + 1;
+        gen = gen == 31 ? 1u : gen + 1;
 #pragma unroll 1
         for (uint32_t j = 1; j <= 8; ++j) {
             const uint32_t cnt = 1u << j;
@@ -321,7 +350,7 @@ struct Fgk {
                 const uint32_t x = pe & 1023u;
                 const uint32_t b = T.body[x];
                 const bool inner = (b & kInner) && (pe >> 10) == j - 1;
-                *(on && inner ? &T.body[x] : scr16()) = (uint16_t)((b & 0x3FFu) | (gen << kMarkShift));
+                *(on && inner ? &T.body[x] : scr16()) = (uint16_t)((b & kContent) | (gen << kMarkShift));
                 const uint32_t ne = inner ? (((b & 255u) * 2 + (q & 1u)) | (j << 10)) : pe;
                 *(on ? &T.lvl[cnt - 2 + q] : scr16()) = (uint16_t)ne;
             }
@@ -336,7 +365,8 @@ struct Fgk {
     {
         const uint32_t t = nyt;
         const uint32_t bpos = lane == 0 ? t : (lane == 1 ? t - 2 : t - 1);
-        const uint32_t bval = lane == 0 ? (kInner | ((t - 2) >> 1)) : (lane == 1 ? kNyt : sym);
+        constexpr uint32_t nl = kDec ? kNotLeaf : 0u;
+        const uint32_t bval = lane == 0 ? (kInner | nl | ((t - 2) >> 1)) : (lane == 1 ? kNyt | nl : sym);
         *(lane < 3 ? &T.body[bpos] : scr16()) = (uint16_t)bval;
         if (!kDec) *(lane == 0 ? &T.where[sym] : scr16()) = (uint16_t)(t - 1);
         if (kWide) *(lane < 2 ? &T.up[t - 2 + lane] : scr16()) = (uint16_t)t;
@@ -360,9 +390,9 @@ struct Fgk {
         const uint32_t b = (lane & 1) ? bs : bl;      // lanes 0/1: content for s / l
         const uint32_t pos = (lane & 1) ? l : s;
         if (kDec) {  // generation marks stay with the positions
-            const uint32_t keep = ((lane & 1) ? bl : bs) & ~0x3FFu;
-            *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & 0x3FFu) | keep);
-            stale += (((bs >> kMarkShift) == gen) | ((bl >> kMarkShift) == gen)) ? kRefresh : 0u;
+            const uint32_t keep = ((lane & 1) ? bl : bs) & (31u << kMarkShift);
+            *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & kContent) | keep);
+            stale += ((((bs >> kMarkShift) & 31u) == gen) | (((bl >> kMarkShift) & 31u) == gen)) ? kRefresh : 0u;
         } else {
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
             *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
@@ -488,8 +518,8 @@ struct Fgk {
     // reported one increment with one store; without a report the root lanes bump the root in
     // the same store. update_fast() is this lane-parallel part; it returns the first reported
     // level (0xFFFFFFFF: none), where walk() continues.
-    // force (wave-uniform, 0 or 0 - 1 / 0 - 2 / 0 - 3): report level 0, store nothing (the
-    // limit becomes all ones, above every weight word and sentinel)
+    // force (wave-uniform, 0 or 0xFFFFFFFF): report level 0, store nothing (the limit becomes
+    // all ones, no weight word or sentinel above it)
     template <class Ahead>
     __device__ __forceinline__ uint32_t update_fast(uint32_t a, Ahead &&ahead, uint32_t force = 0)
     {
@@ -497,9 +527,10 @@ struct Fgk {
         ahead();  // the caller's reads for later symbols go out behind these
         const uint64_t fail = ballot(w1 <= (kWide ? (w0 | force | (force >> 1)) : (w0 | 1023u | force)));
         const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
-        // (measured: an exec-masked store, s_bfm + save/restore of exec instead of this compare
-        // and select, made the encoder 3 % slower)
-        *(lane < k ? &T.wt[a] : scr32()) = w0 + kInc;
+        // lanes below k store: the select runs on a scalar mask (s_bfm_b64), one vector op
+        // (measured: an exec-masked store, s_bfm + save/restore of exec, made the encoder 3 %
+        // slower than a compare and select)
+        *(lds_u32 *)(size_t)sel(below_mask(k), lds_off(&T.wt[a]), lds_off(scr32())) = w0 + kInc;
         __builtin_amdgcn_wave_barrier();
         return k;
     }
@@ -1084,8 +1115,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // the root pad (lvl_root). One read gives the depth (lane 0) and the whole root path
             // (duplicated lanes store the same word); it depends only on the window, so the next
             // code's read goes out as soon as this code's depth is known.
-            const uint32_t vk = min(lane, 9u);
-            uint32_t pr = opaque(fgk.T.lvl[((256u | (uint32_t)(in.win >> 56)) >> vk) - 2]);
+            // ((256 | v) >> k) - 2 = (v >> k) + (256 >> k) - 2, and v >> k = window bits 56 + k..63:
+            // one per-lane shift of the window's high word and one per-lane base; lanes 8 and up
+            // shift by 31 and land on lvl_root[-2 + 0/1] (both the root)
+            const uint32_t vsh = 24 + min(lane, 7u);
+            const uint32_t vbase = lds_off16(&fgk.T.lvl[0]) + 2 * (lane < 8 ? (256u >> lane) - 2 : 0xFFFFFFFEu);
+            auto path_read = [&](uint64_t w) {
+                return opaque(*(const lds_u16 *)(size_t)(vbase + ((uint32_t)(w >> 32) >> vsh) * 2));
+            };
+            uint32_t pr = path_read(in.win);
+            const uint32_t bbase = lds_off16(&fgk.T.body[0]);
             uint32_t d, x, b, pv, k;
             // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
             // both sign bits set, one scalar AND
@@ -1096,14 +1135,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                 const uint32_t e8 = uni(pr);  // the leaf's entry
                 x = e8 & 1023u;
                 d = e8 >> 10;
-                b = opaque(fgk.T.body[x]);
+                b = opaque(*(const lds_u16 *)(size_t)lshl1_add(x, bbase));
                 pv = pr & 1023u;
                 in.win <<= d;
                 in.nwin -= d;  // >= 25
-                const uint32_t prn = opaque(fgk.T.lvl[((256u | (uint32_t)(in.win >> 56)) >> vk) - 2]);
-                // a leaf's body is its symbol; inner / NYT (bits 8, 9): force the failure
-                const uint32_t force = 0u - __builtin_amdgcn_ubfe(b, 8, 2);
-                k = fgk.update_fast(pv, [] {}, force);
+                uint32_t prn;
+                // a leaf's body is its symbol; inner / NYT (bit 15): force the failure
+                const uint32_t force = (uint32_t)__builtin_amdgcn_sbfe((int)b, 15, 1);
+                k = fgk.update_fast(pv, [&] { prn = path_read(in.win); }, force);  // the next code's
                 *so++ = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
                 ++left;
                 if (in.nwin <= 32) in.refill();
