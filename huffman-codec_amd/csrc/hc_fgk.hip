@@ -236,7 +236,9 @@ struct Fgk {
           pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
-        for (uint32_t i = lane; i < kWords; i += 64) T.wt[i] = i > kRoot ? 0xFFFFFFFFu : 0u;
+        // narrow encoder: the last word (above kMissPos) is 0, see update_fast
+        for (uint32_t i = lane; i < kWords; i += 64)
+            T.wt[i] = i > kRoot && (kWide || kDec || i != kWords - 1) ? 0xFFFFFFFFu : 0u;
         if (lane < 2) T.lvl_root[lane] = kRoot;
         for (uint32_t i = lane; i < 516; i += 64) {
             T.body[i] = i == kRoot ? (kDec ? kNyt | kNotLeaf : kNyt) : 0;
@@ -525,12 +527,19 @@ struct Fgk {
     {
         const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
         ahead();  // the caller's reads for later symbols go out behind these
-        const uint64_t fail = ballot(w1 <= (kWide ? (w0 | force | (force >> 1)) : (w0 | 1023u | force)));
+        const uint32_t nv = w0 + kInc;
+        // narrow encoder: w1 < w0 + 1024 reports every level whose next position is not
+        // heavier, and falsely (the walk then decides) only one whose next position is exactly
+        // one heavier with a lower parent field (parents grow with the position in practice: 0
+        // of 600k level tests on a photo stream, 1 of 7.7k on a gradient, slot-form model). The
+        // miss row's sentinel pair (all ones, 0) fails: all ones + 1024 wraps to 1023.
+        const uint64_t fail = ballot(kWide ? (w1 <= (w0 | force | (force >> 1)))
+                                           : (kDec ? (w1 <= (w0 | 1023u | force)) : (w1 < nv)));
         const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
         // lanes below k store: the select runs on a scalar mask (s_bfm_b64), one vector op
         // (measured: an exec-masked store, s_bfm + save/restore of exec, made the encoder 3 %
         // slower than a compare and select)
-        *(lds_u32 *)(size_t)sel(below_mask(k), lds_off(&T.wt[a]), lds_off(scr32())) = w0 + kInc;
+        *(lds_u32 *)(size_t)sel(below_mask(k), lds_off(&T.wt[a]), lds_off(scr32())) = nv;
         __builtin_amdgcn_wave_barrier();
         return k;
     }
