@@ -474,7 +474,11 @@ struct Fgk {
     // lane-parallel read of positions s..s+63, one ballot (the trailing-ones count of
     // "weight == w[s]" is the block leader, highest number first), a swap when the leader is
     // neither s nor its parent, one store.
-    __device__ void walk(uint32_t s)
+    // pv: the root path the update started on (lane k: level k, kRoot lanes above). Once the
+    // walk climbs back onto it (a parent that is one of its positions: the swaps so far moved
+    // only positions below that one), the levels above are finished lane-parallel
+    // (update_from); a level that reports there is walked again.
+    __device__ void walk(uint32_t s, uint32_t pv)
     {
         for (;;) {
             const uint32_t v = T.wt[s + lane];  // sentinels cover s + 63 <= 575
@@ -503,6 +507,12 @@ struct Fgk {
             __builtin_amdgcn_wave_barrier();
             s = max(p, s + 1);
             if (s >= kRoot) break;
+            const uint64_t on = ballot(pv == s);
+            if (on) {
+                const uint32_t k = update_from(pv, ff1(on));
+                if (k == 0xFFFFFFFFu) return;  // the root too
+                s = lane_read(pv, k);
+            }
         }
         bad |= s ^ kRoot;
         const uint32_t r = uni(T.wt[kRoot]) + kInc;
@@ -543,10 +553,23 @@ struct Fgk {
         __builtin_amdgcn_wave_barrier();
         return k;
     }
+    // update_fast for the levels from lane m up (the lanes below are levels already done):
+    // returns the first reported level >= m (0xFFFFFFFF: none, the root lanes bumped the root)
+    __device__ __forceinline__ uint32_t update_from(uint32_t a, uint32_t m)
+    {
+        const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
+        const uint32_t nv = w0 + kInc;
+        const uint64_t lo = below_mask(m);
+        const uint64_t fail = ballot(kWide ? (w1 <= w0) : (kDec ? (w1 <= (w0 | 1023u)) : (w1 < nv))) & ~lo;
+        const uint32_t k = ff1(fail);
+        *(lds_u32 *)(size_t)sel(below_mask(k) & ~lo, lds_off(&T.wt[a]), lds_off(scr32())) = nv;
+        __builtin_amdgcn_wave_barrier();
+        return k;
+    }
     __device__ __forceinline__ void update_path(uint32_t a)
     {
         const uint32_t k = update_fast(a, [] {});
-        if (k != 0xFFFFFFFFu) walk(lane_read(a, k));
+        if (k != 0xFFFFFFFFu) walk(lane_read(a, k), a);
     }
 };
 
@@ -858,7 +881,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
                     ++t;
                     continue;
                 }
-                fgk.walk(lane_read(pv, k));
+                fgk.walk(lane_read(pv, k), pv);
             }
             sink.n = rl;
             if (rl == 64) sink.pack();
@@ -1162,7 +1185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // symbol i - 1 left the loop: the window stands d bits into its code
             b = uni(b);
             if (!(b & (kInner | kNyt))) {  // a leaf whose update reported level k: walk from there
-                fgk.walk(lane_read(pv, k));
+                fgk.walk(lane_read(pv, k), pv);
                 continue;
             }
             // nothing was stored for it
