@@ -978,27 +978,27 @@ struct BitSource {
 // revert is a 4-state machine on the run counter r: in state 3 a symbol is a count (it emits
 // that many copies of the previous symbol, r -> 0), else a literal (r -> r+1 when it repeats the
 // previous symbol and r is 1 or 2, otherwise r -> 1). A symbol's transition is one of two
-// functions on {0..3} (4 x 2 bits); a wave scan of their compositions gives each symbol's
-// state, scans of output lengths and diff sums give each lane's output offset and running byte.
+// functions on {0..3}, a 4-byte table (byte x = f(x)), so a composition is one v_perm_b32; a
+// wave scan of the compositions gives each symbol's state, scans of output lengths and diff
+// sums give each lane's output offset and running byte. Literals write their byte; a lane holds
+// at most one count (counts follow three equal literals, so they are >= 4 symbols apart), and
+// each count's run (an arithmetic sequence mod 256 with the diff model, a constant without)
+// is written by the whole wave, 64 bytes per store.
 struct RevCarry {
     uint32_t r;     // machine state after the last symbol
     uint32_t last;  // last symbol
     uint32_t prev;  // last output byte (diff model)
 };
 
-constexpr uint32_t kFeq = 1u | 2u << 2 | 3u << 4;  // r: 0->1 1->2 2->3 3->0
-constexpr uint32_t kFne = 1u | 1u << 2 | 1u << 4;  // r: 0->1 1->1 2->1 3->0
-constexpr uint32_t kFid = 0u | 1u << 2 | 2u << 4 | 3u << 6;
+constexpr uint32_t kFeq = 1u | 2u << 8 | 3u << 16;  // r: 0->1 1->2 2->3 3->0
+constexpr uint32_t kFne = 1u | 1u << 8 | 1u << 16;  // r: 0->1 1->1 2->1 3->0
+constexpr uint32_t kFid = 0u | 1u << 8 | 2u << 16 | 3u << 24;
 
 __device__ __forceinline__ uint32_t fsm_compose(uint32_t g, uint32_t f)  // x -> g(f(x))
 {
-    uint32_t h = 0;
-    for (uint32_t x = 0; x < 4; ++x) {
-        const uint32_t y = (f >> (2 * x)) & 3u;
-        h |= ((g >> (2 * y)) & 3u) << (2 * x);
-    }
-    return h;
+    return __builtin_amdgcn_perm(0u, g, f);  // byte x = byte f(x) of g
 }
+__device__ __forceinline__ uint32_t fsm_apply(uint32_t f, uint32_t r) { return (f >> (8 * r)) & 255u; }
 
 // lane l holds symbols 4l..4l+3 (m valid); bytes go to the stream's output at pos onwards (the
 // buffer range check drops what is past the capacity); returns the bytes produced
@@ -1019,8 +1019,8 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
         inc = lane >= off ? fsm_compose(inc, g) : inc;
     }
     const uint32_t ex = __shfl_up(inc, 1, 64);
-    uint32_t r = ((lane == 0 ? kFid : ex) >> (2 * cy.r)) & 3u;
-    uint32_t len[4], c[4], tot = 0, ds = 0;
+    uint32_t r = fsm_apply(lane == 0 ? kFid : ex, cy.r);
+    uint32_t len[4], c[4], tot = 0, ds = 0, cnt_b = 4;  // cnt_b: the lane's count symbol (4: none)
     for (uint32_t b = 0; b < 4; ++b) {
         const uint32_t sb = byte_of(x4, b), pb = byte_of(xp, b);
         const bool valid = i0 + b < m;
@@ -1029,7 +1029,8 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
         c[b] = cnt ? pb : sb;
         ds += valid ? (cnt ? sb * pb : sb) : 0u;
         tot += len[b];
-        r = (f[b] >> (2 * r)) & 3u;
+        cnt_b = valid && cnt ? b : cnt_b;
+        r = fsm_apply(f[b], r);
     }
     // exclusive scans of (length, diff sum mod 256), packed: both halves stay below 2^16
     const uint32_t mine = tot | ((ds & 255u) << 16);
@@ -1041,14 +1042,31 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
     const uint32_t exc = acc - mine;
     uint32_t prev = (cy.prev + (exc >> 16)) & 255u;
     uint32_t o = pos + (exc & 0xFFFFu);
+    // literals; the count only records its run: output offset, length | base << 8 | step << 16
+    // (run byte j = base + step * (j + 1); base = the byte before it, or the repeated byte
+    // itself with step 0 without the diff model)
+    uint32_t ro = 0, rlen = 0;
     for (uint32_t b = 0; b < 4; ++b) {
-        for (uint32_t k = 0; k < len[b]; ++k) {
+        if (b == cnt_b) {
+            rlen = dmask ? (len[b] | prev << 8 | c[b] << 16) : (len[b] | c[b] << 8);
+            ro = o;
+            prev = dmask ? (prev + len[b] * c[b]) & 255u : (len[b] ? c[b] : prev);
+        } else {
             prev = ((prev & dmask) + c[b]) & 255u;
-            buf_store8(rs, o++, prev);
+            buf_store8(rs, len[b] ? o : kDrop, prev);
+        }
+        o += len[b];
+    }
+    for (uint64_t runs = ballot((rlen & 255u) != 0); runs; runs &= runs - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(runs);
+        const uint32_t at = lane_read(ro, l), spec = lane_read(rlen, l), n = spec & 255u;
+        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            buf_store8(rs, j < n ? at + j : kDrop, ((spec >> 8) & 255u) + (spec >> 16) * (j + 1));
         }
     }
     const uint32_t all = lane_read(acc, 63);
-    cy.r = (lane_read(inc, 63) >> (2 * cy.r)) & 3u;
+    cy.r = fsm_apply(lane_read(inc, 63), cy.r);
     cy.last = byte_of(lane_read(x4, (m - 1) >> 2), (m - 1) & 3u);
     cy.prev = (cy.prev + (all >> 16)) & 255u;
     return all & 0xFFFFu;
