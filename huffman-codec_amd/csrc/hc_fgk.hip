@@ -76,7 +76,13 @@ constexpr uint32_t kDrop = 0x7FFFFFF8u;         // buffer offset past every rang
 
 constexpr uint32_t kMissPos = kWords - 2;  // sentinel: w[kMissPos + 1] <= w[kMissPos], so it fails
 constexpr uint32_t kSlots = 16;     // encoder path cache: entries
-constexpr uint32_t kSlotDepth = 12; // deepest cached path
+constexpr uint32_t kSlotDepth = 12; // row capacity: levels per cache entry
+#ifndef HC_INSERT_DEPTH
+#define HC_INSERT_DEPTH 9
+#endif
+// deepest path a miss inserts: deeper (rarer) symbols would only evict paths that are used
+// again (slot-form model, photo -c -m: misses 5.84 % at 12, 4.95 % at 9, 5.10 % at 8)
+constexpr uint32_t kInsertDepth = HC_INSERT_DEPTH;
 constexpr uint32_t kRow = 16;       // u16 per cache entry
 constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte chunk, <= 342
                                     // (a byte emits 2 only at a run start that follows a run of
@@ -287,7 +293,7 @@ struct Fgk {
     // streams this misses less than a clock with reference bits, and a hit costs nothing).
     __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t rec)
     {
-        if (d > kSlotDepth) return;
+        if (d > kInsertDepth) return;
         uint32_t e;
         if (pc_free) {
             e = (uint32_t)__builtin_ctz(pc_free);
@@ -817,7 +823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         // bit k = code bit (position parity, left = even) of level k; read MSB first it is the
         // root-to-leaf code (the kRoot lanes are even)
         const uint64_t bits = ballot(pv & 1u);
-        if (d <= kSlotDepth) fgk.pc_insert(sym, s, pv, d, (1u << d) | (uint32_t)bits);
+        if (d <= kInsertDepth) fgk.pc_insert(sym, s, pv, d, (1u << d) | (uint32_t)bits);
         fgk.update_path(pv);
         if (fresh) {
             // the path starts at the new leaf, one level below the NYT whose code is sent
