@@ -41,6 +41,9 @@ namespace {
 __device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t lane)
 {
     uint64_t *const tr = g_trace;
+#ifdef HC_PROF
+    return;  // the buffer holds the path profile (prof_store)
+#endif
     if (tr == nullptr) return;
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     uint32_t hw, xcc;
@@ -51,6 +54,24 @@ __device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t l
         tr[3 * sid + 1] = t1;
         tr[3 * sid + 2] = (hw & 0xFFFFu) | ((xcc & 0xFu) << 16);
     }
+}
+
+// Diagnostic build (-DHC_PROF, scripts/path_prof.py): lane i of a per-wave accumulator sums the
+// s_memtime cycles spent in region i of the kernel; at the end lanes 0..7 go to g_trace[8 *
+// stream + i], lane 0 holding the wave's whole life. Absent from normal builds.
+#ifdef HC_PROF
+#define HC_PROF_BEGIN() const uint64_t hc_p0_ = __builtin_amdgcn_s_memtime()
+#define HC_PROF_END(i) (pacc += lane == (i) ? __builtin_amdgcn_s_memtime() - hc_p0_ : 0)
+#else
+#define HC_PROF_BEGIN()
+#define HC_PROF_END(i)
+#endif
+__device__ __forceinline__ void prof_store(uint32_t sid, uint64_t t0, uint64_t pacc, uint32_t lane)
+{
+#ifdef HC_PROF
+    uint64_t *const tr = g_trace;
+    if (tr != nullptr && lane < 8) tr[8 * sid + lane] = lane == 0 ? __builtin_amdgcn_s_memtime() - t0 : pacc;
+#endif
 }
 
 // The issue arbiter prefers higher priority, then older waves: left alone, the oldest of a
@@ -770,6 +791,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
     if (sid >= bt.n) return;
+    uint64_t pacc = 0;  // HC_PROF regions
+    (void)pacc;
 
     const uint64_t in_off = uni64(bt.in_offs[sid]);
     const uint64_t n = uni64(bt.in_lens[sid]);
@@ -819,12 +842,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         const uint32_t fresh = s == 0;
         if (fresh) s = uni(fgk.split(sym));
         uint32_t pv;
-        const uint32_t d = fgk.chase(s, pv);
+        uint32_t d;
+        {
+            HC_PROF_BEGIN();
+            d = fgk.chase(s, pv);
+            HC_PROF_END(5);
+        }
         // bit k = code bit (position parity, left = even) of level k; read MSB first it is the
         // root-to-leaf code (the kRoot lanes are even)
         const uint64_t bits = ballot(pv & 1u);
         if (d <= kInsertDepth) fgk.pc_insert(sym, s, pv, d, (1u << d) | (uint32_t)bits);
-        fgk.update_path(pv);
+        {
+            HC_PROF_BEGIN();
+            fgk.update_path(pv);
+            HC_PROF_END(6);
+        }
         if (fresh) {
             // the path starts at the new leaf, one level below the NYT whose code is sent
             // (huffman.cpp:44-50): drop that lowest bit, then 8 raw bits
@@ -883,14 +915,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
                 if (lane_read(pv, 0) == kMissPos) {
                     --t;
                     sink.n = rl - 1;  // its record lane, overwritten by the miss path
+                    HC_PROF_BEGIN();
                     miss(sb[t]);
+                    HC_PROF_END(1);
                     ++t;
                     continue;
                 }
+                HC_PROF_BEGIN();
                 fgk.walk(lane_read(pv, k), pv);
+                HC_PROF_END(2);
             }
             sink.n = rl;
-            if (rl == 64) sink.pack();
+            if (rl == 64) {
+                HC_PROF_BEGIN();
+                sink.pack();
+                HC_PROF_END(3);
+            }
         }
     };
 
@@ -910,8 +950,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
             continue;
         }
         // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
+        HC_PROF_BEGIN();
         const uint32_t ns = rle_chunk<kSrc>(chunk, m, base + m == n32 ? 1u : 0u, cy, fgk.T.syms,
                                             fgk.scr32(), lane);
+        HC_PROF_END(4);
         code_all(ns);
         nsym += ns;
     }
@@ -926,6 +968,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         bt.status[sid] = (int32_t)st;
     }
     trace_wave(sid, t0, lane);
+    prof_store(sid, t0, pacc, lane);
 }
 
 // --------------------------------------------------------------------------- the decoder --
@@ -1087,6 +1130,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
     if (sid >= bt.n) return;
+    uint64_t pacc = 0;  // HC_PROF regions
+    (void)pacc;
 
     const uint64_t in_off = uni64(bt.in_offs[sid]);
     const uint64_t len = uni64(bt.in_lens[sid]);
@@ -1157,7 +1202,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
             // where the walk from the root stops (depth d <= 8), the levels above give the
             // positions the walk passes.
-            if (fgk.stale >= kRefresh) fgk.build_levels();
+            if (fgk.stale >= kRefresh) {
+                HC_PROF_BEGIN();
+                fgk.build_levels();
+                HC_PROF_END(5);
+            }
             if (in.nwin <= 32) in.refill();
             // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
             // symbol's depth is known the next symbol's table entry is read, before this
@@ -1209,11 +1258,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // symbol i - 1 left the loop: the window stands d bits into its code
             b = uni(b);
             if (!(b & (kInner | kNyt))) {  // a leaf whose update reported level k: walk from there
+                HC_PROF_BEGIN();
                 fgk.walk(lane_read(pv, k), pv);
+                HC_PROF_END(1);
                 continue;
             }
             // nothing was stored for it
             uint32_t sym = 0;
+            HC_PROF_BEGIN();
             if (b & kInner) {
                 // the code is longer than the tables reach, or they stopped short (a leaf that
                 // split since): descend bit by bit, top-down first (depth j at lane 64-j),
@@ -1247,7 +1299,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                     fgk.chase(known, pv);
                 }
             }
-            if (!(b & kInner)) fgk.update_path(pv);
+            HC_PROF_END(2);
+            if (!(b & kInner)) {
+                HC_PROF_BEGIN();
+                fgk.update_path(pv);
+                HC_PROF_END(3);
+            }
             sbuf[i - 1 - i0] = (uint8_t)sym;
         }
         __builtin_amdgcn_wave_barrier();
@@ -1258,7 +1315,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                 buf_store8(rout, lane * 4 + b < m ? pos + lane * 4 + b : kDrop, byte_of(x4, b));
             pos += m;
         } else {
+            HC_PROF_BEGIN();
             pos += revert_block(x4, m, rc, dmask, rout, pos, lane);
+            HC_PROF_END(4);
         }
     }
     if (consumed() > payload_bits) st = HC_ERR_HUFFMAN;  // ran past the payload
@@ -1270,6 +1329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
         bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? pos : 0;
     }
     trace_wave(sid, t0, lane);
+    prof_store(sid, t0, pacc, lane);
 }
 
 }  // namespace
