@@ -61,6 +61,28 @@ def analyze(name, tr):
           f"waves started after another ended on the same SIMD: mean {sum(rounds) / len(rounds) - 1:.2f}; "
           f"mean wave life {life / n:.3g} cycles, launch span on XCD 0 {span0:.3g} cycles; wave life / the "
           f"SIMD's longest, by rank: {rel}", flush=True)
+    # balance across SIMDs (s_memtime counts per XCD: compare within one): per SIMD, when its
+    # first wave started and its last ended, relative to the XCD's first start, as fractions of
+    # the XCD's span; and the spread of wave lives over the streams
+    for xcc in sorted({r[2] >> 16 for r in tr.tolist()})[:2]:
+        rows = [r for r in tr.tolist() if (r[2] >> 16) == xcc]
+        t0 = min(r[0] for r in rows)
+        span = max(r[1] for r in rows) - t0
+        first = collections.defaultdict(lambda: float("inf"))
+        last = collections.defaultdict(float)
+        for a, b, hw in rows:
+            first[hw & ~0xF] = min(first[hw & ~0xF], a)
+            last[hw & ~0xF] = max(last[hw & ~0xF], b)
+        def pct(v):
+            v = sorted(v)
+            return " ".join(f"{v[int(q * (len(v) - 1))]:.3f}" for q in (0, 0.1, 0.5, 0.9, 1))
+        print(f"  XCD {xcc}: span {span:.3g}; SIMD first start / span (min p10 p50 p90 max): "
+              f"{pct([(x - t0) / span for x in first.values()])}; SIMD last end / span: "
+              f"{pct([(x - t0) / span for x in last.values()])}", flush=True)
+    lives = sorted(b - a for a, b, _ in tr.tolist())
+    m = sum(lives) / len(lives)
+    print(f"  wave life / mean (min p10 p50 p90 max): " + " ".join(
+        f"{lives[int(q * (len(lives) - 1))] / m:.3f}" for q in (0, 0.1, 0.5, 0.9, 1)), flush=True)
 
 
 def main():
