@@ -413,28 +413,27 @@ struct Fgk {
         // encoder: drop the cached paths through s or l first; the relink below then gives a
         // moved leaf's where[] its new position
         if (!kDec) pc_swapped(s, l);
-        const uint32_t bs = uni(T.body[s]);
-        const uint32_t bl = uni(T.body[l]);
-        const uint32_t k = lane >> 1;                 // 0: content going to s, 1: to l
-        const uint32_t b = (lane & 1) ? bs : bl;      // lanes 0/1: content for s / l
-        const uint32_t pos = (lane & 1) ? l : s;
-        if (kDec) {  // generation marks stay with the positions
-            const uint32_t keep = ((lane & 1) ? bl : bs) & (31u << kMarkShift);
-            *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & kContent) | keep);
-            stale += ((((bs >> kMarkShift) & 31u) == gen) | (((bl >> kMarkShift) & 31u) == gen)) ? kRefresh : 0u;
+        // lane-parallel: lane & 1 = 0 handles the content moving to s (read at l), 1 the one
+        // moving to l; lanes 2, 3 (lane >> 1 = 1) re-parent the second child of the same content
+        const uint32_t pos = (lane & 1) ? l : s;        // where the lane's content goes
+        const uint32_t b = T.body[(lane & 1) ? s : l];  // that content
+        if (kDec) {
+            // generation marks stay with the positions: the destination's own word is the
+            // partner lane's read (quad_perm [1,0,3,2])
+            const uint32_t bo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);
+            *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & kContent) | (bo & (31u << kMarkShift)));
+            stale += ballot(lane < 2 && ((b >> kMarkShift) & 31u) == gen) ? kRefresh : 0u;
         } else {
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
             *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
         }
-        const uint32_t cb = k ? bs : bl;              // lanes 0..3: content whose child moves
-        const uint32_t cpos = k ? l : s;
-        const bool inner = lane < 4 && (cb & kInner);
-        const uint32_t c = (cb & 255u) * 2 + (lane & 1);
+        const bool inner = lane < 4 && (b & kInner);
+        const uint32_t c = (b & 255u) * 2 + (lane >> 1);
         if (kWide) {
-            *(inner ? &T.up[c] : scr16()) = (uint16_t)cpos;
+            *(inner ? &T.up[c] : scr16()) = (uint16_t)pos;
         } else {
             uint32_t *q = inner ? &T.wt[c] : scr32();
-            *q = (*q & ~1023u) | cpos;
+            *q = (*q & ~1023u) | pos;
         }
         __builtin_amdgcn_wave_barrier();
     }
