@@ -257,6 +257,7 @@ struct Fgk {
     uint32_t stale;    // decoder: >= kRefresh = rebuild the level tables (a swap moved a position
                        // they walk through: += kRefresh; a lookup they left short: += 1)
     const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
+    uint64_t pacc = 0;        // HC_PROF regions inside the tree code
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
         : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), gen(0), stale(kRefresh),
@@ -412,7 +413,11 @@ struct Fgk {
     {
         // encoder: drop the cached paths through s or l first; the relink below then gives a
         // moved leaf's where[] its new position
-        if (!kDec) pc_swapped(s, l);
+        if (!kDec) {
+            HC_PROF_BEGIN();
+            pc_swapped(s, l);
+            HC_PROF_END(7);
+        }
         // lane-parallel: lane & 1 = 0 handles the content moving to s (read at l), 1 the one
         // moving to l; lanes 2, 3 (lane >> 1 = 1) re-parent the second child of the same content
         const uint32_t pos = (lane & 1) ? l : s;        // where the lane's content goes
@@ -967,7 +972,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         bt.status[sid] = (int32_t)st;
     }
     trace_wave(sid, t0, lane);
-    prof_store(sid, t0, pacc, lane);
+    prof_store(sid, t0, pacc + fgk.pacc, lane);
 }
 
 // --------------------------------------------------------------------------- the decoder --
@@ -1328,7 +1333,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
         bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? pos : 0;
     }
     trace_wave(sid, t0, lane);
-    prof_store(sid, t0, pacc, lane);
+    prof_store(sid, t0, pacc + fgk.pacc, lane);
 }
 
 }  // namespace

@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "huffman-codec_amd", "python"))
 
 ENC = {1: "miss (chase, insert, update, push)", 5: "  of which: chase", 6: "  of which: update (walk)",
-       2: "walk after a failed leader test", 3: "record pack", 4: "MNP-5 chunk pass"}
+       2: "walk after a failed leader test", 3: "record pack", 4: "MNP-5 chunk pass",
+       7: "  of which (any walk): cache scan per swap"}
 DEC = {1: "walk after a failed leader test", 2: "long code descent / NYT", 3: "update after descent / NYT",
        4: "RLE + diff revert", 5: "level table rebuild"}
 
