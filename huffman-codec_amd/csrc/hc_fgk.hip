@@ -505,10 +505,12 @@ struct Fgk {
     // lane-parallel read of positions s..s+63, one ballot (the trailing-ones count of
     // "weight == w[s]" is the block leader, highest number first), a swap when the leader is
     // neither s nor its parent, one store.
-    // pv: the root path the update started on (lane k: level k, kRoot lanes above). Once the
-    // walk climbs back onto it (a parent that is one of its positions: the swaps so far moved
-    // only positions below that one), the levels above are finished lane-parallel
-    // (update_from); a level that reports there is walked again.
+    // pv: the root path the update started on (lane k: level k, kRoot lanes above). After the
+    // level at s, the climb from its parent is chased (one LDS read per position, no leader
+    // test) until it meets a position of pv -- every swap so far moved only positions below
+    // that one, and pv's kRoot lanes end any climb at the root. The chased positions and pv
+    // above the meeting point are the rest of the root path, finished lane-parallel like
+    // update_fast; a level that reports there is walked again, the new path taking pv's role.
     __device__ void walk(uint32_t s, uint32_t pv)
     {
         for (;;) {
@@ -536,19 +538,25 @@ struct Fgk {
             }
             *(lane == 0 ? dst : scr32()) = nv;
             __builtin_amdgcn_wave_barrier();
-            s = max(p, s + 1);
-            if (s >= kRoot) break;
-            const uint64_t on = ballot(pv == s);
-            if (on) {
-                const uint32_t k = update_from(pv, ff1(on));
-                if (k == 0xFFFFFFFFu) return;  // the root too
-                s = lane_read(pv, k);
+            // chase from the parent until a position of pv; lane j of td: the j-th one passed
+            uint32_t c = p, n = 0, td = kRoot;
+            uint64_t on;
+            while ((on = ballot(pv == c)) == 0) {
+                td = writelane(td, c, n);
+                if (++n > c) {  // parents sit above children: more levels than the position is a bug
+                    bad = 1;
+                    return;
+                }
+                c = kWide ? uni(T.up[c]) : (uni(T.wt[c]) & 1023u);
             }
+            // lane j < n: chased; lane j >= n: pv's lane j - n + m (kRoot past its lane 63)
+            const uint32_t src = lane - n + ff1(on);
+            const uint32_t up = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)pv);
+            pv = lane < n ? td : (src < 64 ? up : kRoot);
+            const uint32_t k = update_from(pv, 0);
+            if (k == 0xFFFFFFFFu) return;  // the root too
+            s = lane_read(pv, k);
         }
-        bad |= s ^ kRoot;
-        const uint32_t r = uni(T.wt[kRoot]) + kInc;
-        *(lane == 0 ? &T.wt[kRoot] : scr32()) = r;
-        __builtin_amdgcn_wave_barrier();
     }
 
     // The same update when the path is already known: lanes 0..d-1 hold the positions of
