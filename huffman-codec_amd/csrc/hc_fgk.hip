@@ -264,9 +264,10 @@ struct Fgk {
           pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
-        // narrow encoder: the last word (above kMissPos) is 0, see update_fast
+        // narrow: sentinels above every weight word; the encoder's last word (above kMissPos)
+        // is 0 and the decoder's are all ones - 1, see update_fast
         for (uint32_t i = lane; i < kWords; i += 64)
-            T.wt[i] = i > kRoot && (kWide || kDec || i != kWords - 1) ? 0xFFFFFFFFu : 0u;
+            T.wt[i] = i <= kRoot ? 0u : (kWide ? 0xFFFFFFFFu : (kDec ? 0xFFFFFFFEu : (i != kWords - 1 ? 0xFFFFFFFFu : 0u)));
         if (lane < 2) T.lvl_root[lane] = kRoot;
         for (uint32_t i = lane; i < 516; i += 64) {
             T.body[i] = i == kRoot ? (kDec ? kNyt | kNotLeaf : kNyt) : 0;
@@ -570,20 +571,21 @@ struct Fgk {
     // the same store. update_fast() is this lane-parallel part; it returns the first reported
     // level (0xFFFFFFFF: none), where walk() continues.
     // force (wave-uniform, 0 or 0xFFFFFFFF): report level 0, store nothing (the limit becomes
-    // all ones, no weight word or sentinel above it)
+    // all ones, above every weight word and sentinel)
     template <class Ahead>
     __device__ __forceinline__ uint32_t update_fast(uint32_t a, Ahead &&ahead, uint32_t force = 0)
     {
         const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
         ahead();  // the caller's reads for later symbols go out behind these
         const uint32_t nv = w0 + kInc;
-        // narrow encoder: w1 < w0 + 1024 reports every level whose next position is not
-        // heavier, and falsely (the walk then decides) only one whose next position is exactly
-        // one heavier with a lower parent field (parents grow with the position in practice: 0
-        // of 600k level tests on a photo stream, 1 of 7.7k on a gradient, slot-form model). The
-        // miss row's sentinel pair (all ones, 0) fails: all ones + 1024 wraps to 1023.
-        const uint64_t fail = ballot(kWide ? (w1 <= (w0 | force | (force >> 1)))
-                                           : (kDec ? (w1 <= (w0 | 1023u | force)) : (w1 < nv)));
+        // narrow: w1 < w0 + 1024 (the increment stored anyway) reports every level whose next
+        // position is not heavier, and falsely (the walk then decides) only one whose next
+        // position is exactly one heavier with a lower parent field (parents grow with the
+        // position in practice: 0 of 600k level tests on a photo stream, 1 of 7.7k on a
+        // gradient, slot-form model). The encoder's miss row's sentinel pair (all ones, 0)
+        // fails: all ones + 1024 wraps to 1023; the decoder's force makes the limit all ones,
+        // above its sentinels (all ones - 1).
+        const uint64_t fail = ballot(kWide ? (w1 <= (w0 | force | (force >> 1))) : (w1 < (nv | force)));
         const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
         // lanes below k store: the select runs on a scalar mask (s_bfm_b64), one vector op
         // (measured: an exec-masked store, s_bfm + save/restore of exec, made the encoder 3 %
@@ -599,7 +601,7 @@ struct Fgk {
         const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
         const uint32_t nv = w0 + kInc;
         const uint64_t lo = below_mask(m);
-        const uint64_t fail = ballot(kWide ? (w1 <= w0) : (kDec ? (w1 <= (w0 | 1023u)) : (w1 < nv))) & ~lo;
+        const uint64_t fail = ballot(kWide ? (w1 <= w0) : (w1 < nv)) & ~lo;
         const uint32_t k = ff1(fail);
         *(lds_u32 *)(size_t)sel(below_mask(k) & ~lo, lds_off(&T.wt[a]), lds_off(scr32())) = nv;
         __builtin_amdgcn_wave_barrier();
