@@ -234,3 +234,60 @@ def run(symbols):
     n = max(1, len(symbols))
     return dict(n=len(symbols), enc_hit=enc["hits"] / n, inval=enc["inval"] / n,
                 rebuilds=pt.rebuilds / n, cont=pt.cont / n, bits=len(bits))
+
+
+# ---- the kernels' update (hc_fgk.hip: update_fast / update_from / walk), on the same slot tree.
+# The lane-parallel test works on the narrow weight words (weight << 10 | parent): a level is
+# reported unless word(p + 1) >= word(p) + 1024, which never passes a non-leader and reports
+# falsely only for the NYT's parent or a next position one heavier with a lower parent field.
+# The walk does one exact level, then chases the climb back onto the known path (no leader
+# test) and finishes the rest lane-parallel again.
+
+def _word(t, p):
+    return (t.w[p] << 10) | (t.up[p] if p < ROOT else 0) if p <= ROOT else (1 << 62)
+
+
+def lanes_update(t, path, m=0):
+    """update_from(path, m): path = positions of levels m.. (ROOT last); returns the first
+    reported index or None (then every level incl. the root was incremented)"""
+    k = None
+    for j in range(m, len(path)):
+        p = path[j]
+        if p != ROOT and not _word(t, p + 1) >= _word(t, p) + 1024:
+            k = j
+            break
+    for j in range(m, len(path) if k is None else k):
+        t.w[path[j]] += 1
+    return k
+
+
+def kernel_walk(t, s, pv):
+    """walk(s, pv): pv = the known root path, ROOT last"""
+    while True:
+        f = t.w[s]
+        lead = s
+        while t.w[lead + 1] == f:
+            lead += 1
+        if lead != s and lead != t.up[s]:
+            a, c = t.body[s], t.body[lead]
+            t.body[s], t.body[lead] = c, a
+            t.relink(c, s)
+            t.relink(a, lead)
+            s = lead
+        t.w[s] += 1
+        c, td = t.up[s], []
+        while c not in pv:
+            td.append(c)
+            c = t.up[c]
+        path = td + pv[pv.index(c):]
+        k = lanes_update(t, path)
+        if k is None:
+            return
+        s, pv = path[k], path
+
+
+def kernel_update(t, x, pv):
+    """update_path: pv = t.path(x) + [ROOT]"""
+    k = lanes_update(t, pv)
+    if k is not None:
+        kernel_walk(t, pv[k], pv)

@@ -50,3 +50,32 @@ def test_cache_model_edges():
     M.run([5])
     M.run([5] * 300)
     M.run(list(range(256)) * 3)
+
+
+def _lockstep(symbols):
+    """The kernels' update (lane-parallel test, walk with chase-back) leaves exactly the tree
+    of the plain slot-form update after every symbol."""
+    ref, ker = M.Tree(), M.Tree()
+    for s in symbols:
+        for t in (ref, ker):
+            if t.where[s] == 0:
+                t.split(s)
+        x = ref.where[s]
+        assert ker.where[s] == x
+        ref.update(x)
+        M.kernel_update(ker, x, ker.path(x) + [M.ROOT])
+        assert ref.w == ker.w and ref.body == ker.body and ref.up == ker.up
+
+
+def test_kernel_update_streams(oracle_mod):
+    for name, sym in _streams(oracle_mod):
+        _lockstep(list(sym))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_kernel_update_random(seed):
+    rng = random.Random(100 + seed)
+    alphabet = list(range(256))
+    weights = [1.0 / (1 + i) ** rng.choice([0.5, 1.2, 2.0]) for i in range(256)]
+    rng.shuffle(alphabet)
+    _lockstep(rng.choices(alphabet, weights, k=5000))
