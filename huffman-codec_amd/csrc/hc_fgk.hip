@@ -868,7 +868,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
         if (d <= kInsertDepth) fgk.pc_insert(sym, s, pv, d, (1u << d) | (uint32_t)bits);
         {
             HC_PROF_BEGIN();
-            fgk.update_path(pv);
+            // a path too deep to cache belongs to a rare symbol, whose leaf nearly always ties
+            // with the next position (9 in 10 on the slot-form model): walk from the leaf at once
+            if (d > kInsertDepth) fgk.walk(s, pv);
+            else fgk.update_path(pv);
             HC_PROF_END(6);
         }
         if (fresh) {
@@ -1279,6 +1282,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             }
             // nothing was stored for it
             uint32_t sym = 0;
+            bool deep = false;  // a code longer than the cache's 9 levels: a rare symbol
             HC_PROF_BEGIN();
             if (b & kInner) {
                 // the code is longer than the tables reach, or they stopped short (a leaf that
@@ -1296,6 +1300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                     b = uni(fgk.T.body[x]);
                 } while ((b & kInner) && depth < 63);
                 if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
+                deep = depth > kInsertDepth;
                 pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
                 pv = lane < depth ? pv : kRoot;
                 sym = b & 255u;
@@ -1316,7 +1321,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             HC_PROF_END(2);
             if (!(b & kInner)) {
                 HC_PROF_BEGIN();
-                fgk.update_path(pv);
+                // a rare symbol's leaf nearly always ties with the next position (9 in 10 on
+                // the slot-form model): walk from the leaf at once
+                if (deep) fgk.walk(lane_read(pv, 0), pv);
+                else fgk.update_path(pv);
                 HC_PROF_END(3);
             }
             sbuf[i - 1 - i0] = (uint8_t)sym;
