@@ -253,6 +253,8 @@ struct Fgk {
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
     uint32_t pc_next;  // encoder: FIFO hand of the path cache
     uint32_t pc_free;  // encoder: entries dropped by swaps (or never used), taken first
+    uint32_t pc_lb;    // encoder: a weight no cached path's position is below (pc_bound)
+    uint32_t pc_lb_ok; // encoder: no insert since pc_bound
     uint32_t gen;      // decoder: generation of the level tables
     uint32_t stale;    // decoder: >= kRefresh = rebuild the level tables (a swap moved a position
                        // they walk through: += kRefresh; a lookup they left short: += 1)
@@ -260,7 +262,7 @@ struct Fgk {
     uint64_t pacc = 0;        // HC_PROF regions inside the tree code
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
-        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), gen(0), stale(kRefresh),
+        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), pc_lb(0), pc_lb_ok(0), gen(0), stale(kRefresh),
           pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
@@ -317,6 +319,7 @@ struct Fgk {
     __device__ __forceinline__ void pc_insert(uint32_t sym, uint32_t s, uint32_t pv, uint32_t d, uint32_t rec)
     {
         if (d > kInsertDepth) return;
+        pc_lb_ok = 0;
         uint32_t e;
         if (pc_free) {
             e = (uint32_t)__builtin_ctz(pc_free);
@@ -331,6 +334,23 @@ struct Fgk {
         const uint32_t rv = lane < kSlotDepth ? pv : (lane == kSlotDepth ? rec : (d | 32u | (sym << 8)));
         *(lane < kSlotDepth + 2 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)rv;
         __builtin_amdgcn_wave_barrier();
+    }
+
+    // pc_lb := the lightest cached leaf. Every position on a cached path weighs at least its
+    // leaf and weights only grow, so until the next insert a swap of positions lighter than
+    // that (the ties of rare symbols) touches no cached path and needs no scan.
+    __device__ __forceinline__ void pc_bound()
+    {
+        if (pc_lb_ok) return;
+        pc_lb_ok = 1;
+        const uint32_t p0 = T.pc[(lane & (kSlots - 1)) * kRow];  // row (lane & 15)'s leaf
+        const uint32_t w0 = T.wt[min(p0, kRoot)];
+        uint32_t lw = p0 <= kRoot ? (kWide ? w0 : w0 >> 10) : 0xFFFFFFFFu;  // 0xFFFF: unused row
+        lw = min(lw, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)lw, 0x111, 0xF, 0xF, false));
+        lw = min(lw, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)lw, 0x112, 0xF, 0xF, false));
+        lw = min(lw, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)lw, 0x114, 0xF, 0xF, false));
+        lw = min(lw, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)lw, 0x118, 0xF, 0xF, false));
+        pc_lb = lane_read(lw, 15);
     }
 
     __device__ void pc_drop(uint32_t e)
@@ -410,11 +430,11 @@ struct Fgk {
     // huffman.cpp:186-217 in slot form: exchange the contents of positions s and l (their
     // weights are equal), then re-point what hangs below them. Lane k < 2 writes the content
     // moving into (k ? l : s); lane k < 4 re-parents child (k & 1) of content (k >> 1).
-    __device__ __forceinline__ void swap(uint32_t s, uint32_t l)
+    __device__ __forceinline__ void swap(uint32_t s, uint32_t l, bool scan)
     {
-        // encoder: drop the cached paths through s or l first; the relink below then gives a
-        // moved leaf's where[] its new position
-        if (!kDec) {
+        // encoder: drop the cached paths through s or l first (scan: they may lie on one); the
+        // relink below then gives a moved leaf's where[] its new position
+        if (!kDec && scan) {
             HC_PROF_BEGIN();
             pc_swapped(s, l);
             HC_PROF_END(7);
@@ -512,7 +532,9 @@ struct Fgk {
     // that one, and pv's kRoot lanes end any climb at the root. The chased positions and pv
     // above the meeting point are the rest of the root path, finished lane-parallel like
     // update_fast; a level that reports there is walked again, the new path taking pv's role.
-    __device__ void walk(uint32_t s, uint32_t pv)
+    // bounded: the encoder's pc_lb is current (pc_bound since the last insert): swaps below it
+    // skip the cache scan
+    __device__ void walk(uint32_t s, uint32_t pv, bool bounded = false)
     {
         for (;;) {
             const uint32_t v = T.wt[s + lane];  // sentinels cover s + 63 <= 575
@@ -526,7 +548,7 @@ struct Fgk {
                 const uint32_t lead =
                     ~le ? s + (uint32_t)__builtin_ctzll(~le) - 1 : leader_far(s + 64, ws);
                 if (lead != p) {
-                    swap(s, lead);
+                    swap(s, lead, !kDec && (!bounded || (kWide ? ws : ws >> 10) >= pc_lb));
                     // the swap rewrites only parent fields below s and lead, never their own
                     // words, so the pre-swap read still holds lead's word when in range
                     const uint32_t off = lead - s;
@@ -870,7 +892,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
             HC_PROF_BEGIN();
             // a path too deep to cache belongs to a rare symbol, whose leaf nearly always ties
             // with the next position (9 in 10 on the slot-form model): walk from the leaf at once
-            if (d > kInsertDepth) fgk.walk(s, pv);
+            if (d > kInsertDepth) {
+                fgk.pc_bound();
+                fgk.walk(s, pv, true);
+            }
             else fgk.update_path(pv);
             HC_PROF_END(6);
         }
