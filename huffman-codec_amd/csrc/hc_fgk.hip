@@ -191,7 +191,6 @@ __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t l
     return (uint32_t)amdgcn_writelane((int)x, (int)l, (int)v);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ bool any(bool p) { return ballot(p) != 0; }
 // lowest set bit of a wave mask, 0xFFFFFFFF for 0 (s_ff1_i32_b64 without the zero test)
 __device__ __forceinline__ uint32_t ff1(uint64_t m)
 {
