@@ -169,14 +169,6 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x)
     asm("" : "+v"(x));
     return x;
 }
-// bits 56..63 of a wave-uniform u64, computed on the vector unit (a VGPR): the address it
-// feeds is then one v_lshl_add, not three scalar ops and a copy
-__device__ __forceinline__ uint32_t top8(uint64_t w)
-{
-    uint32_t r;
-    asm("v_lshrrev_b32 %0, 24, %1" : "=v"(r) : "s"((uint32_t)(w >> 32)));
-    return r;
-}
 __device__ __forceinline__ uint32_t lane_id()
 {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
