@@ -26,6 +26,11 @@ sys.path.insert(0, os.path.join(ROOT, "huffman-codec_amd", "python"))
 
 METRIC = "encode+decode GiB/s on batched 512×512 .raw, 1/2/4/8 GPUs; bit-exact check"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# what bounds the FGK kernels: VALU + SALU instruction issue per CU at their occupancy (8 waves
+# per SIMD), measured by scripts/micro/issue.hip (independent VALU 1.77, VALU:SALU 1:1 1.73,
+# SALU alone 0.95 instructions / cycle / CU)
+ISSUE_PEAK = 1.75
+CLOCK_HZ = 2.4e9
 N_RAW = 512 * 512
 
 
@@ -198,6 +203,22 @@ def main():
             t = json.load(f)
         key = f"{dom}:{'cm' if use_diff else 'c'}:{args.kind}:{S}"
         traffic = t.get(key)
+    # the issue bound of the dominant kernel, from its PMC instruction counts (profiles/, same
+    # workload only) over this run's launch time
+    issue = None
+    ppath = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+    if use_diff and args.kind == "photo" and S == 8192 and os.path.exists(ppath):
+        with open(ppath) as f:
+            pm = json.load(f)
+        ps = pm.get("per_symbol", {}).get({"encode_kernel": "encode_kernel<narrow,raw+diff>",
+                                           "decode_kernel": "decode_kernel<narrow,raw>"}[dom])
+        if ps:
+            per_cu = (ps["SQ_INSTS_VALU"] + ps["SQ_INSTS_SALU"]) * pm["symbols_per_launch"] / 256
+            ach = per_cu / (dom_ms * 1e-3 * CLOCK_HZ)
+            issue = {"bound": "VALU+SALU issue", "kernel": dom, "achieved": round(ach, 3), "peak": ISSUE_PEAK,
+                     "unit": "instructions/cycle/CU", "frac": round(ach / ISSUE_PEAK, 3),
+                     "source": "profiles/r01_pmc_summary.json (SQ_INSTS_VALU+SQ_INSTS_SALU per symbol), "
+                               "peak: scripts/micro/issue.hip"}
     result = {
         "metric": METRIC, "value": round(value, 4), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
@@ -210,6 +231,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
+        "issue": issue,
         "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
         "encode_GiBps": round(world * S * N_RAW / (enc_ms * 1e-3) / 2**30, 4),
         "decode_GiBps": round(world * S * N_RAW / (dec_ms * 1e-3) / 2**30, 4),
