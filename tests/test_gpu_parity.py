@@ -72,6 +72,43 @@ def test_batch_vs_oracle_mixed_sizes(gpu, hc, oracle_mod):
         assert st == [0] * len(raws) and back == raws
 
 
+def _deep_and_skewed():
+    """Symbol streams that stress the tree rather than the transforms: Fibonacci counts (codes
+    deeper than the decoder's 8 table levels and the encoder's cached paths, up to the
+    reference's ~24-bit worst case), a Zipf alphabet (hot cached symbols among many cold ones:
+    swaps that drop cache entries), all 256 symbols round robin (a flat tree, no repeats for
+    the first 256 symbols), two symbols alternating (swap every symbol), sorted runs."""
+    rng = np.random.default_rng(23)
+    out = []
+    for n_fib in (12, 20, 24):
+        sym, a, b = [], 1, 1
+        for s in range(n_fib):
+            sym += [(s * 37) & 255] * a
+            a, b = b, a + b
+        sym = np.array(sym, dtype=np.uint8)
+        out.append(sym.tobytes())                   # ascending counts, unshuffled
+        out.append(rng.permutation(sym).tobytes())  # the same counts shuffled
+    zipf = 1.0 / np.arange(1, 257) ** 1.1
+    out.append(rng.choice(256, 150000, p=zipf / zipf.sum()).astype(np.uint8).tobytes())
+    out.append(bytes(range(256)) * 300)
+    out.append(b"\x00\xff" * 40000)
+    out.append(np.repeat(np.arange(256, dtype=np.uint8), 200).tobytes())
+    return out
+
+
+def test_batch_deep_and_skewed(gpu, hc, oracle_mod):
+    torch = gpu
+    raws = _deep_and_skewed()
+    for use_diff in (False, True):
+        st, encs, _ = compress_batch(hc, torch, raws, use_diff)
+        assert st == [0] * len(raws)
+        for i, (r, e) in enumerate(zip(raws, encs)):
+            ost, want = oracle_mod.compress(r, use_diff, False, 512)
+            assert ost == 0 and e == want, (i, len(r), use_diff)
+        st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
+        assert st == [0] * len(raws) and back == raws
+
+
 def test_batch_edge_vectors(gpu, hc, vectors):
     torch = gpu
     for mode in ("c", "cm"):
