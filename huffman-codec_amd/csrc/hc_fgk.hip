@@ -247,13 +247,14 @@ struct Fgk {
     uint32_t pc_lb;    // encoder: a weight no cached path's position is below (pc_bound)
     uint32_t pc_lb_ok; // encoder: no insert since pc_bound
     uint32_t gen;      // decoder: generation of the level tables
-    uint32_t stale;    // decoder: >= kRefresh = rebuild the level tables (a swap moved a position
-                       // they walk through: += kRefresh; a lookup they left short: += 1)
+    uint32_t stale;    // decoder: lookups the level tables left short (kRefresh: from := 0)
+    uint32_t from;     // decoder: rebuild levels from..8 of the tables (9: none, 0: all, in a new
+                       // generation); a swap moved a position they reach at level from - 1
     const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
     uint64_t pacc = 0;        // HC_PROF regions inside the tree code
 
     __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
-        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), pc_lb(0), pc_lb_ok(0), gen(0), stale(kRefresh),
+        : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), pc_lb(0), pc_lb_ok(0), gen(0), stale(0), from(0),
           pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
@@ -379,11 +380,19 @@ struct Fgk {
     // j-bit prefix is where the walk from the root along those bits stops (position | depth <<
     // 10); built breadth first, each level from the one above. A swap stales them only when it
     // moves the content of a position some walk passes through: those carry the generation.
+    // from = 0: all levels, a new generation; otherwise levels from..8 (the entries above reach
+    // neither swapped position, so they and the marks they set stand)
     __device__ void build_levels()
     {
-        gen = gen == 31 ? 1u : gen + 1;
+        uint32_t j0 = from;
+        if (j0 == 0) {
+            gen = gen == 31 ? 1u : gen + 1;
+            j0 = 1;
+            stale = 0;
+        }
+        from = 9;
 #pragma unroll 1
-        for (uint32_t j = 1; j <= 8; ++j) {
+        for (uint32_t j = j0; j <= 8; ++j) {
             const uint32_t cnt = 1u << j;
             for (uint32_t r = 0; r * 64 < cnt; ++r) {
                 const uint32_t q = lane + 64 * r;
@@ -398,7 +407,22 @@ struct Fgk {
             }
             __builtin_amdgcn_wave_barrier();
         }
-        stale = 0;
+    }
+
+    // decoder: the shallowest level < 8 whose entries hold position s or l (8 if none does).
+    // Level j's entries sit at 2^j - 2 .. 2^(j+1) - 3 and a position first appears at its
+    // depth, so the lowest matching index names it (level 8's entries stay right: a position
+    // they stop at is walked on by the descent). Entries of levels >= from may predate a swap
+    // earlier in this walk; a match there gives a level >= from - 1, leaving from as it is.
+    __device__ uint32_t table_level(uint32_t s, uint32_t l)
+    {
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t i = r * 64 + lane;
+            const uint32_t p = T.lvl[i] & 1023u;
+            const uint64_t m = ballot(i < 254 && (p == s || p == l));
+            if (m) return 31 - __builtin_clz(r * 64 + ff1(m) + 2);
+        }
+        return 8;
     }
 
     // huffman.cpp:99-111: split NYT at t -> NYT at t-2 (left), symbol leaf at t-1 (right).
@@ -439,7 +463,7 @@ struct Fgk {
             // partner lane's read (quad_perm [1,0,3,2])
             const uint32_t bo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & kContent) | (bo & (31u << kMarkShift)));
-            stale += ballot(lane < 2 && ((b >> kMarkShift) & 31u) == gen) ? kRefresh : 0u;
+            if (ballot(lane < 2 && ((b >> kMarkShift) & 31u) == gen)) from = min(from, table_level(s, l) + 1);
         } else {
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
             *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
@@ -1235,7 +1259,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
             // where the walk from the root stops (depth d <= 8), the levels above give the
             // positions the walk passes.
-            if (fgk.stale >= kRefresh) {
+            if (fgk.from < 9) {
                 HC_PROF_BEGIN();
                 fgk.build_levels();
                 HC_PROF_END(5);
@@ -1307,6 +1331,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                 uint32_t depth = uni(d);
                 x = uni(x);
                 fgk.stale += depth < 8 ? 1u : 0u;
+                if (fgk.stale >= kRefresh) fgk.from = 0;
                 // levels 1..8 of the prefix, lane 64 - j <- level j (lane 8 - j of the path read)
                 uint32_t pt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 56) & 63u) * 4), (int)pv);
                 do {

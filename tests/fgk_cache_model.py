@@ -132,19 +132,24 @@ class PathCache:
 class LevelTables:
     """L_j[p] for j = 1..8 and every j-bit prefix p: (position, depth) where the walk from the root
     along p's bits stops (a leaf above depth j keeps its entry). Built breadth first, one level
-    at a time, as the kernel does; `through` = inner positions some walk passes (depth < 8)."""
+    at a time, as the kernel does; `through` = inner positions some walk passes (depth < 8): the
+    kernel's generation marks, which a partial rebuild adds to and only a full one clears."""
 
     def __init__(self):
-        self.L = {}
+        self.L = {0: [(ROOT, 0)]}
         self.through = set()
-        self.dirty = True
+        self.frm = 0  # rebuild levels frm..8 (9: none, 0: all)
         self.short = 0
         self.rebuilds = self.cont = 0
 
     def build(self, t):
-        self.through = set()
-        prev = [(ROOT, 0)]
-        for j in range(1, 9):
+        j0 = self.frm
+        if j0 == 0:
+            self.through = set()
+            self.short = 0
+            j0 = 1
+        prev = self.L[j0 - 1]
+        for j in range(j0, 9):
             cur = []
             for q in range(1 << j):
                 x, dep = prev[q >> 1]
@@ -155,17 +160,25 @@ class LevelTables:
                     cur.append((x, dep))
             self.L[j] = cur
             prev = cur
-        self.dirty = False
-        self.short = 0
+        self.frm = 9
         self.rebuilds += 1
+
+    def table_level(self, s, lead):
+        """the shallowest level < 8 holding position s or lead (8: none), scanning entries in
+        index order as the kernel's table_level does"""
+        for j in range(1, 8):
+            if any(x in (s, lead) for x, _ in self.L[j]):
+                return j
+        return 8
 
     def on_swap(self, s, lead):
         if s in self.through or lead in self.through:
-            self.dirty = True  # a walk through s or lead changed: the tables are wrong
+            # a walk through s or lead changed: levels deeper than either's are wrong
+            self.frm = min(self.frm, self.table_level(s, lead) + 1)
 
     def lookup(self, t, bits, i):
         """-> (leaf position, depth, root path bottom-up)"""
-        if self.dirty or self.short >= REFRESH:
+        if self.frm < 9:
             self.build(t)
         v = 0
         for k in range(8):
@@ -176,6 +189,8 @@ class LevelTables:
             self.cont += 1
             if d < 8:
                 self.short += 1  # the tables stop short of depth 8 here: refresh them soon
+                if self.short >= REFRESH:
+                    self.frm = 0
             while t.body[x] & INNER:
                 x = (t.body[x] & 255) * 2 + bits[i + d]
                 d += 1
