@@ -104,6 +104,11 @@ constexpr uint32_t kSlotDepth = 12; // row capacity: levels per cache entry
 // deepest path a miss inserts: deeper (rarer) symbols would only evict paths that are used
 // again (slot-form model, photo -c -m: misses 5.84 % at 12, 4.95 % at 9, 5.10 % at 8)
 constexpr uint32_t kInsertDepth = HC_INSERT_DEPTH;
+#ifndef HC_PROBE
+#define HC_PROBE 7
+#endif
+// encoder: a miss chases this many levels, then looks the position reached up in the path cache
+constexpr uint32_t kProbe = HC_PROBE;
 constexpr uint32_t kRow = 16;       // u16 per cache entry
 constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte chunk, <= 342
                                     // (a byte emits 2 only at a run start that follows a run of
@@ -519,7 +524,46 @@ struct Fgk {
         int32_t km = -64;       // levels - 64
         uint32_t s = vreg(s0);  // per-level work on the VALU (see vreg)
         uint32_t td = kRoot;    // lane j: level k - 1 - j
-        do {
+        if (!kDec) {
+            // encoder: kProbe levels, then look the position up in the path cache: a cached
+            // path through it (rows stay valid paths) gives the rest of the climb at once
+#pragma unroll
+            for (uint32_t i = 0; i < kProbe; ++i) {
+                const uint32_t sh = __builtin_amdgcn_update_dpp(0u, td, 0x138, 0xF, 0xF, true);
+                td = lane == 0 ? s : sh;
+                ++km;
+                s = kWide ? (uint32_t)T.up[s] : (T.wt[s] & 1023u);
+                if (uni(s) == kRoot) break;
+            }
+            const uint32_t c = uni(s);
+            if (c != kRoot) {
+                constexpr uint64_t kLevels = 0x0FFF0FFF0FFF0FFFull;
+                uint32_t q[kSlots / 4];
+                uint64_t m[kSlots / 4];
+#pragma unroll
+                for (uint32_t r = 0; r < kSlots / 4; ++r) q[r] = T.pc[64 * r + lane];
+#pragma unroll
+                for (uint32_t r = 0; r < kSlots / 4; ++r) m[r] = ballot(q[r] == c) & kLevels;
+                const uint64_t m01 = m[0] | m[1], m23 = m[2] | m[3];
+                if (m01 | m23) {
+                    // the first hit: entry e, level lv of its row
+                    const uint32_t r = m01 ? (m[0] ? 0u : 1u) : (m[2] ? 2u : 3u);
+                    const uint32_t b = ff1(r == 0 ? m[0] : r == 1 ? m[1] : r == 2 ? m[2] : m[3]);
+                    const uint32_t e = 4 * r + (b >> 4), lv = b & 15u;
+                    const uint32_t n = (uint32_t)(km + 64);  // levels chased: c is level n
+                    // lane j >= n: level j = the row's level lv + j - n (kRoot from the row's
+                    // depth on, and past its 12 levels)
+                    const uint32_t idx = lv + lane - n;
+                    const uint32_t rv = T.pc[e * kRow + min(idx, kRow - 1)];
+                    const uint32_t drow = uni(T.pc[e * kRow + kSlotDepth + 1]) & 31u;
+                    const uint32_t dn =
+                        (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((n - 1 - lane) & 63u) * 4), (int)td);
+                    pv = lane < n ? dn : (idx < kSlotDepth ? rv : kRoot);
+                    return n + drow - lv;
+                }
+            }
+        }
+        if (kDec || uni(s) != kRoot) do {
             // wave_shr:1, lane 0 taking s
             const uint32_t sh = __builtin_amdgcn_update_dpp(0u, td, 0x138, 0xF, 0xF, true);
             td = lane == 0 ? s : sh;
