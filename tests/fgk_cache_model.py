@@ -96,7 +96,7 @@ class PathCache:
         self.ent = [None] * SLOTS  # (sym, pv)
         self.slot = {}             # sym -> slot
         self.next = 0
-        self.hits = self.misses = self.inval = 0
+        self.hits = self.misses = self.inval = self.probes = 0
 
     def lookup(self, sym):
         e = self.slot.get(sym)
@@ -120,6 +120,23 @@ class PathCache:
             self.slot.pop(self.ent[e][0], None)
         self.ent[e] = (sym, list(pv))
         self.slot[sym] = e
+
+    def probe(self, t, x, levels=7):
+        """The encoder's miss chase (hc_fgk.hip: chase + pc_probe): climb `levels` levels from
+        x, then take the rest of the root path from the first entry (lowest number, then lowest
+        level) whose path holds the position reached. None: the climb reached the root or no
+        entry holds it (the kernel then chases on)."""
+        up, c = [], x
+        for _ in range(levels):
+            up.append(c)
+            c = t.up[c]
+            if c == ROOT:
+                return None
+        for e in range(SLOTS):
+            if self.ent[e] is not None and c in self.ent[e][1]:
+                row = self.ent[e][1]
+                return up + row[row.index(c):]
+        return None
 
     def on_swap(self, s, lead):
         for e in range(SLOTS):
@@ -212,6 +229,9 @@ def run(symbols):
         pv = pc.lookup(sym)
         true = t.path(x)
         if pv is None:
+            probed = pc.probe(t, x)
+            assert probed is None or probed == true, (sym, probed, true)
+            pc.probes += probed is not None
             pv = true
             pc.insert(sym, pv)
         assert pv == true, (sym, pv, true)
@@ -220,7 +240,7 @@ def run(symbols):
         t.update(x)
         for s, lead in t.swaps:
             pc.on_swap(s, lead)
-    enc = dict(hits=pc.hits, misses=pc.misses, inval=pc.inval)
+    enc = dict(hits=pc.hits, misses=pc.misses, inval=pc.inval, probes=pc.probes)
 
     t = Tree()
     pt = LevelTables()
@@ -247,7 +267,7 @@ def run(symbols):
             pt.on_swap(s, lead)
     assert out == list(symbols) and i == len(bits)
     n = max(1, len(symbols))
-    return dict(n=len(symbols), enc_hit=enc["hits"] / n, inval=enc["inval"] / n,
+    return dict(n=len(symbols), enc_hit=enc["hits"] / n, probe_hit=enc["probes"] / n, inval=enc["inval"] / n,
                 rebuilds=pt.rebuilds / n, cont=pt.cont / n, bits=len(bits))
 
 
