@@ -113,7 +113,10 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte chunk, <= 342
                                     // (a byte emits 2 only at a run start that follows a run of
                                     // >= 3, so such bytes are >= 3 apart)
-constexpr uint32_t kRefresh = 16;   // decoder: rebuild the level tables after this many lookups
+#ifndef HC_REFRESH
+#define HC_REFRESH 16
+#endif
+constexpr uint32_t kRefresh = HC_REFRESH;   // decoder: rebuild the level tables after this many lookups
                                     // they left short of depth 8
 constexpr uint32_t kMarkShift = 10; // decoder: body bits 10..14 = table generation (per position)
 constexpr uint32_t kNotLeaf = 0x8000; // decoder: body bit 15 = inner or NYT (moves with the content)
