@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
 """bench.py — encode+decode GiB/s of the MI355X huffman-codec on batched 512x512 .raw streams.
 
-Workload (BASELINE.json configs[4], weak-scaled): every GPU owns a shard of S = 8192 synthetic
-512x512 photo streams (seed 0x5EED, stream k = rank*S + j, generated in
-HBM), and one step is the reference's full round trip on that shard: `-c -m` encode
+Headline workload = BASELINE.json configs[4] (C5): a batch of 65536 synthetic 512x512 photo
+streams (seed 0x5EED, generated in HBM), sharded across the ranks
+(strong scaling: rank r owns streams [r*S, (r+1)*S), S = 65536 / N; at N=1 the GPU codes the
+whole C5 batch). One step is the reference's full round trip on the shard: `-c -m` encode
 (diff -> MNP-5 RLE -> FGK -> header, one fused kernel) then decode (FGK -> RLE revert -> diff
-revert, one fused kernel). value = raw bytes of all ranks / step time (max over ranks), in
-GiB/s. Decoded output is checked against the input (bit-exact) after the timed region.
+revert, one fused kernel). value = raw bytes of all ranks / step time (max over ranks), GiB/s.
+After the timed region: every status 0, decode == input on every stream, and (rank 0, N=1) the
+first streams' encodings byte-identical to the reference binary's own output for them.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Streams are independent, so ranks share nothing on the data path (scaling "weak"); after the
-timed region RCCL all-reduces the verification counters and all-gathers the encoded sizes.
+At N=1 the same JSON line also carries "configs": the other BASELINE.json configs measured in
+the same run (C2 one stream, C3 4096 streams `-c`, C4 the 4096x4096 adaptive matrix, and the
+grad / noise distributions of SURVEY.md §8d), each checked against the reference's digests
+(tests/golden/digests.json) or by round trip, each with its own roofline line.
+
+Streams are independent, so ranks share nothing on the data path; after the timed region RCCL
+all-reduces the verification counters and the max step time.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -32,6 +40,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 ISSUE_PEAK = 1.75
 CLOCK_HZ = 2.4e9
 N_RAW = 512 * 512
+C5_STREAMS = 65536
+PMC_PATH = os.path.join(ROOT, "profiles", "pmc_summary.json")
+FGK_SRC = os.path.join(ROOT, "huffman-codec_amd", "csrc", "hc_fgk.hip")
 
 
 def parse():
@@ -39,73 +50,253 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--streams", type=int, default=8192, help="streams per GPU")
+    ap.add_argument("--streams", type=int, default=C5_STREAMS, help="streams in the whole batch (all ranks)")
     ap.add_argument("--kind", default="photo", choices=["photo", "grad", "noise"])
     ap.add_argument("--no-diff", action="store_true", help="-c instead of -c -m")
     ap.add_argument("--cpu-sample", type=int, default=0, help="streams for the CPU baseline (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
-    ap.add_argument("--gather", action="store_true",
-                    help="after timing, gather every rank's encoded payloads into rank 0")
+    ap.add_argument("--no-configs", action="store_true", help="N=1: skip the other BASELINE configs")
+    ap.add_argument("--only-configs", default="", help="comma list: run just these configs (no headline)")
     return ap.parse_args()
 
 
-def cpu_baseline(args, cores):
-    """The reference binary itself (oracle/_ref, Makefile flags) on a bounded sample of the
-    same workload, one process per stream over `cores` host cores; falls back to the oracle's
-    C restatement (kind "port") when the binary was not shipped."""
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def src_sha():
+    with open(FGK_SRC, "rb") as f:
+        return sha(f.read())[:16]
+
+
+def cpu_baseline(args, cores, gpu_encoded):
+    """The reference binary itself (oracle/_ref: the Makefile build, -O0, and the same sources
+    at -O2) on a bounded sample of the same workload, one process per stream over `cores` host
+    cores. The sample is rank 0's first streams, so the reference's .huf files are also compared
+    byte for byte with the GPU's encodings of the same streams (gpu_encoded)."""
     import subprocess
     from concurrent.futures import ThreadPoolExecutor
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
-    sample = args.cpu_sample or 8 * cores
-    kind = "reference" if oracle.ref_available() else "port"
+    sample = min(args.cpu_sample or 8 * cores, len(gpu_encoded))
     raws = [oracle.synth(args.kind, k).tobytes() for k in range(sample)]
     mode = ["-c"] if args.no_diff else ["-c", "-m"]
-    tmp = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
-    try:
-        for i, r in enumerate(raws):
-            with open(os.path.join(tmp, f"{i}.raw"), "wb") as f:
-                f.write(r)
+    legs = []
+    for label, binary in (("-O2", oracle.REF_BIN_O2), ("Makefile -O0", oracle.REF_BIN)):
+        if not os.path.exists(binary):
+            continue
+        tmp = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        try:
+            for i, r in enumerate(raws):
+                with open(os.path.join(tmp, f"{i}.raw"), "wb") as f:
+                    f.write(r)
 
-        def enc(i):
-            if kind == "reference":
-                subprocess.run([oracle.REF_BIN] + mode + ["-i", f"{i}.raw", "-o", f"{i}.huf"], cwd=tmp,
-                               check=True, capture_output=True)
-            else:
-                st, out = oracle.compress(raws[i], not args.no_diff, False, 512)
-                with open(os.path.join(tmp, f"{i}.huf"), "wb") as f:
-                    f.write(out)
-
-        def dec(i):
-            if kind == "reference":
-                subprocess.run([oracle.REF_BIN, "-d", "-i", f"{i}.huf", "-o", f"{i}.out"], cwd=tmp, check=True,
+            def enc(i):
+                subprocess.run([binary] + mode + ["-i", f"{i}.raw", "-o", f"{i}.huf"], cwd=tmp, check=True,
                                capture_output=True)
-            else:
-                with open(os.path.join(tmp, f"{i}.huf"), "rb") as f:
-                    st, out = oracle.decompress(f.read())
-                with open(os.path.join(tmp, f"{i}.out"), "wb") as f:
-                    f.write(out)
 
-        with ThreadPoolExecutor(cores) as ex:
-            t0 = time.perf_counter()
-            list(ex.map(enc, range(sample)))
-            t1 = time.perf_counter()
-            list(ex.map(dec, range(sample)))
-            t2 = time.perf_counter()
-        ok = all(open(os.path.join(tmp, f"{i}.out"), "rb").read() == raws[i] for i in range(sample))
-    finally:
-        for fn in os.listdir(tmp):
-            os.remove(os.path.join(tmp, fn))
-        os.rmdir(tmp)
-    total = sample * N_RAW
-    return {"value": total / (t2 - t0) / 2**30, "unit": "GiB/s", "cores": cores, "kind": kind,
-            "sample": f"{sample} x 512x512 {args.kind} streams, {' '.join(mode)} then -d, one process per "
-                      f"stream on {cores} host cores ({'oracle/_ref/huffman-codec, reference Makefile flags -O0' if kind == 'reference' else 'oracle C restatement'})",
-            "encode_GiBps": total / (t1 - t0) / 2**30, "decode_GiBps": total / (t2 - t1) / 2**30,
-            "seconds": t2 - t0, "bit_exact": ok}
+            def dec(i):
+                subprocess.run([binary, "-d", "-i", f"{i}.huf", "-o", f"{i}.out"], cwd=tmp, check=True,
+                               capture_output=True)
+
+            with ThreadPoolExecutor(cores) as ex:
+                t0 = time.perf_counter()
+                list(ex.map(enc, range(sample)))
+                t1 = time.perf_counter()
+                list(ex.map(dec, range(sample)))
+                t2 = time.perf_counter()
+            rt = all(open(os.path.join(tmp, f"{i}.out"), "rb").read() == raws[i] for i in range(sample))
+            same = all(open(os.path.join(tmp, f"{i}.huf"), "rb").read() == gpu_encoded[i] for i in range(sample))
+        finally:
+            for fn in os.listdir(tmp):
+                os.remove(os.path.join(tmp, fn))
+            os.rmdir(tmp)
+        total = sample * N_RAW
+        legs.append({"build": label, "value": total / (t2 - t0) / 2**30, "encode_GiBps": total / (t1 - t0) / 2**30,
+                     "decode_GiBps": total / (t2 - t1) / 2**30, "seconds": t2 - t0, "round_trip": rt,
+                     "gpu_bytes_identical": same})
+    if not legs:
+        return None
+    main_leg = legs[0]
+    return {"value": main_leg["value"], "unit": "GiB/s", "cores": cores, "kind": "reference",
+            "build": main_leg["build"],
+            "sample": f"{sample} x 512x512 {args.kind} streams (k = 0..{sample - 1}), {' '.join(mode)} then -d, "
+                      f"one process per stream on {cores} host cores (oracle/_ref, compiled from the reference "
+                      f"sources; value = the {main_leg['build']} build, every build in legs)",
+            "legs": legs,
+            "bit_exact_vs_gpu": all(l["gpu_bytes_identical"] and l["round_trip"] for l in legs)}
+
+
+class Batch:
+    """S synthetic 512x512 streams resident in HBM with encode / decode buffers."""
+
+    def __init__(self, torch, hc, dev, kind, k0, S, use_diff, side=512):
+        self.torch, self.hc, self.dev, self.S, self.use_diff = torch, hc, dev, S, use_diff
+        self.N = side * side
+        N = self.N
+        self.cap = 2 * N + 4096
+        self.raw = torch.empty(S * N, dtype=torch.uint8, device=dev)
+        hc.synth_batch(kind, k0, S, side, side, self.raw, N)
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.offs = torch.arange(S, **i64) * N
+        self.lens = torch.full((S,), N, **i64)
+        self.enc = torch.empty(S * self.cap, dtype=torch.uint8, device=dev)
+        self.eoffs = torch.arange(S, **i64) * self.cap
+        self.ecaps = torch.full((S,), self.cap, **i64)
+        self.elens = torch.zeros(S, **i64)
+        self.est = torch.zeros(S, dtype=torch.int32, device=dev)
+        self.back = torch.empty_like(self.raw)
+        self.blens = torch.zeros_like(self.lens)
+        self.bst = torch.zeros_like(self.est)
+
+    def step(self, stream, ev=None):
+        hc = self.hc
+        if ev is not None:
+            ev[0].record(stream)
+        hc.compress_batch(self.raw, self.offs, self.lens, self.enc, self.eoffs, self.ecaps, self.elens,
+                          self.est, use_diff=self.use_diff, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        hc.decompress_batch(self.enc, self.eoffs, self.elens, self.back, self.offs, self.lens, self.blens,
+                            self.bst, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    def bad(self):
+        torch = self.torch
+        b = int((self.est != 0).sum() + (self.bst != 0).sum() + (self.blens != self.lens).sum())
+        return b + (0 if torch.equal(self.back, self.raw) else 1)
+
+    def encoded(self, k):
+        n = int(self.elens[k])
+        o = k * self.cap
+        return self.enc[o:o + n].cpu().numpy().tobytes()
+
+
+def timed(torch, b, stream, steps, warmup, barrier=None):
+    """warmup + `steps` timed round trips; returns (wall seconds, enc ms, dec ms per launch)"""
+    for _ in range(warmup):
+        b.step(stream)
+    torch.cuda.synchronize(b.dev)
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    if barrier:
+        barrier()
+    torch.cuda.synchronize(b.dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        b.step(stream, events[k])
+    torch.cuda.synchronize(b.dev)
+    if barrier:
+        barrier()
+    t1 = time.perf_counter()
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / steps
+    return t1 - t0, enc_ms, dec_ms
+
+
+def roofline(S, N, enc_bytes, enc_ms, dec_ms, mode, kind):
+    """the dominant kernel: algorithmic bytes per launch (raw read + encoded written for encode,
+    encoded read + raw written for decode) / its average launch time (HIP events
+    on the launch stream); traffic = PMC HBM bytes per launch from profiles/pmc_summary.json when
+    that file was measured on this exact kernel source and workload"""
+    alg = S * N + enc_bytes
+    dom, ms = ("decode_kernel", dec_ms) if dec_ms >= enc_ms else ("encode_kernel", enc_ms)
+    ach = alg / (ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBPS, 6), "traffic": None, "alg_bytes_per_launch": alg,
+         "avg_launch_ms": round(ms, 4)}
+    issue = None
+    if os.path.exists(PMC_PATH):
+        with open(PMC_PATH) as f:
+            pm = json.load(f)
+        key = f"{dom}:{mode}:{kind}:{S}"
+        e = pm.get("launches", {}).get(key)
+        if e and pm.get("source_sha") == src_sha():
+            r["traffic"] = e.get("hbm_bytes")
+            r["traffic_source"] = f"profiles/pmc_summary.json[{key}] (rocprofv3 PMC, same kernel source)"
+            if "valu_salu_insts" in e:
+                ach_i = e["valu_salu_insts"] / 256 / (ms * 1e-3 * CLOCK_HZ)
+                issue = {"bound": "VALU+SALU issue", "kernel": dom, "achieved": round(ach_i, 3), "peak": ISSUE_PEAK,
+                         "unit": "instructions/cycle/CU", "frac": round(ach_i / ISSUE_PEAK, 3),
+                         "source": f"SQ_INSTS_VALU+SQ_INSTS_SALU per launch from profiles/pmc_summary.json[{key}]; "
+                                   "peak: scripts/micro/issue.hip"}
+    return r, issue
+
+
+def config_batch(torch, hc, dev, stream, name, what, kind, S, use_diff, steps, digests, side=512):
+    b = Batch(torch, hc, dev, kind, 0, S, use_diff, side)
+    wall, enc_ms, dec_ms = timed(torch, b, stream, steps, 1)
+    bad = b.bad()
+    mode = "cm" if use_diff else "c"
+    enc_bytes = int(b.elens.sum())
+    out = {"what": what, "streams": S, "mode": "-c -m" if use_diff else "-c", "kind": kind,
+           "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+           "GiBps": round(S * b.N / ((enc_ms + dec_ms) * 1e-3) / 2**30, 4),
+           "encode_GiBps": round(S * b.N / (enc_ms * 1e-3) / 2**30, 4),
+           "decode_GiBps": round(S * b.N / (dec_ms * 1e-3) / 2**30, 4),
+           "bits_per_byte": round(enc_bytes * 8 / (S * b.N), 4), "round_trip_exact": bad == 0}
+    # the reference's digests for streams k = 0..3 of this kind (512x512)
+    if side == 512 and digests:
+        ok = True
+        for k in range(min(S, 4)):
+            want = digests["synthetic"][f"{kind}_{k}"][mode]
+            got = b.encoded(k)
+            ok &= (len(got), sha(got)) == (want["len"], want["sha256"])
+        out["reference_digests_identical"] = bool(ok)
+        bad += 0 if ok else 1
+    out["roofline"], out["issue"] = roofline(S, b.N, enc_bytes, enc_ms, dec_ms, mode, kind)
+    del b
+    torch.cuda.empty_cache()
+    return out, bad
+
+
+def config_c4(torch, hc, digests):
+    """C4: -c -a -w 4096 (and -c -a -m) on one 4096x4096 photo matrix, single-buffer API (host
+    buffers: the wall time includes the H2D / D2H copies)"""
+    dev = torch.device("cuda", 0)
+    buf = torch.empty(4096 * 4096, dtype=torch.uint8, device=dev)
+    hc.synth_batch("photo", 0, 1, 4096, 4096, buf, 0)
+    torch.cuda.synchronize()
+    raw = buf.cpu().numpy().tobytes()
+    del buf
+    res, bad = {}, 0
+    e = digests["synthetic_4096"]["photo_0"]
+    for mode, d in (("ca", False), ("cma", True)):
+        t0 = time.perf_counter()
+        st, out = hc.compress(raw, d, True, 4096)
+        t1 = time.perf_counter()
+        st2, back = hc.decompress(out)
+        t2 = time.perf_counter()
+        ident = st == 0 and (len(out), sha(out)) == (e[mode]["len"], e[mode]["sha256"])
+        rt = st2 == 0 and back == raw
+        bad += (0 if ident else 1) + (0 if rt else 1)
+        res[mode] = {"what": f"4096x4096 photo {'-c -a -m' if d else '-c -a'} -w 4096, single-buffer API incl. PCIe",
+                     "encode_s": round(t1 - t0, 4), "decode_s": round(t2 - t1, 4), "bytes": len(out),
+                     "reference_digest_identical": ident, "round_trip_exact": rt}
+    return res, bad
+
+
+def run_configs(torch, hc, dev, stream, only):
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        digests = json.load(f)
+    plan = [
+        ("C2", "1 x 512x512 photo -c -m: one stream, one wavefront (latency)", "photo", 1, True, 3),
+        ("C3", "4096 x 512x512 photo -c", "photo", 4096, False, 3),
+        ("grad", "8192 x 512x512 grad -c -m (best case: runs collapse the symbols)", "grad", 8192, True, 3),
+        ("noise", "2048 x 512x512 noise -c -m (worst case: ~262k deep codes per stream)", "noise", 2048, True, 2),
+    ]
+    res, bad = {}, 0
+    for name, what, kind, S, d, steps in plan:
+        if only and name not in only:
+            continue
+        res[name], b = config_batch(torch, hc, dev, stream, name, what, kind, S, d, steps, digests)
+        bad += b
+    if not only or "C4" in only:
+        res["C4"], b = config_c4(torch, hc, digests)
+        bad += b
+    return res, bad
 
 
 def main():
@@ -124,129 +315,71 @@ def main():
     dev = torch.device("cuda", local)
     if not hc.device_ok():
         raise SystemExit("libhcodec.so: no usable gfx950 device")
-
-    S = args.streams
-    use_diff = not args.no_diff
-    cap = 2 * N_RAW + 4096
-    raw = torch.empty(S * N_RAW, dtype=torch.uint8, device=dev)
-    hc.synth_batch(args.kind, rank * S, S, 512, 512, raw, N_RAW)
-    offs = torch.arange(S, dtype=torch.int64, device=dev) * N_RAW
-    lens = torch.full((S,), N_RAW, dtype=torch.int64, device=dev)
-    enc = torch.empty(S * cap, dtype=torch.uint8, device=dev)
-    eoffs = torch.arange(S, dtype=torch.int64, device=dev) * cap
-    ecaps = torch.full((S,), cap, dtype=torch.int64, device=dev)
-    elens = torch.zeros(S, dtype=torch.int64, device=dev)
-    est = torch.zeros(S, dtype=torch.int32, device=dev)
-    back = torch.empty_like(raw)
-    blens = torch.zeros_like(lens)
-    bst = torch.zeros_like(est)
     stream = torch.cuda.current_stream(dev)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, est, use_diff=use_diff, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        hc.decompress_batch(enc, eoffs, elens, back, offs, lens, blens, bst, stream=stream)
-        if ev is not None:
-            ev[2].record(stream)
+    if args.only_configs:
+        res, bad = run_configs(torch, hc, dev, stream, set(args.only_configs.split(",")))
+        print(json.dumps({"configs": res, "bad": bad}), flush=True)
+        raise SystemExit(1 if bad else 0)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    if args.streams % world:
+        raise SystemExit(f"--streams {args.streams} does not split over {world} ranks")
+    S = args.streams // world
+    use_diff = not args.no_diff
+    b = Batch(torch, hc, dev, args.kind, rank * S, S, use_diff)
+    barrier = dist.barrier if world > 1 else None
+    wall, enc_ms, dec_ms = timed(torch, b, stream, args.steps, args.warmup, barrier)
 
     # verification (outside the timed region): every status 0, exact sizes, exact bytes
-    bad = int((est != 0).sum() + (bst != 0).sum() + (blens != lens).sum())
-    bad += 0 if torch.equal(back, raw) else 1
-    enc_bytes = int(elens.sum())
-    elapsed = hcdist.reduce_counters([t1 - t0], op="max", device=dev)
+    bad = b.bad()
+    enc_bytes = int(b.elens.sum())
+    elapsed = hcdist.reduce_counters([wall], op="max", device=dev)
     bad, enc_total = (int(v) for v in hcdist.reduce_counters([bad, enc_bytes], device=dev))
-    sizes = hcdist.gather_sizes(elens)  # every stream's encoded size, on every rank
-    gather_ms = None
-    if args.gather:  # the encoded payloads of all ranks into rank 0 (RCCL all-gather)
-        torch.cuda.synchronize(dev)
-        g0 = time.perf_counter()
-        packed, _ = hcdist.gather_encoded(enc, eoffs, elens)
-        torch.cuda.synchronize(dev)
-        gather_ms = (time.perf_counter() - g0) * 1e3
-        if rank == 0 and packed.numel() != int(sizes.sum()):
-            bad += 1
     if bad:
         raise SystemExit(f"bit-exact check FAILED on {bad} items")
 
     step_s = float(elapsed) / args.steps
     raw_total = world * S * N_RAW
     value = raw_total / step_s / 2**30
-    # roofline of the dominant kernel: algorithmic bytes per launch (raw read + encoded written
-    # for encode, encoded read + raw written for decode) / its average launch time
-    alg_bytes = S * N_RAW + enc_bytes  # this rank, per launch
-    dom, dom_ms = ("decode_kernel", dec_ms) if dec_ms >= enc_ms else ("encode_kernel", enc_ms)
-    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = args.traffic or os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            t = json.load(f)
-        key = f"{dom}:{'cm' if use_diff else 'c'}:{args.kind}:{S}"
-        traffic = t.get(key)
-    # the issue bound of the dominant kernel, from its PMC instruction counts (profiles/, same
-    # workload only) over this run's launch time
-    issue = None
-    ppath = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
-    if use_diff and args.kind == "photo" and S == 8192 and os.path.exists(ppath):
-        with open(ppath) as f:
-            pm = json.load(f)
-        ps = pm.get("per_symbol", {}).get({"encode_kernel": "encode_kernel<narrow,raw+diff>",
-                                           "decode_kernel": "decode_kernel<narrow,raw>"}[dom])
-        if ps:
-            per_cu = (ps["SQ_INSTS_VALU"] + ps["SQ_INSTS_SALU"]) * pm["symbols_per_launch"] / 256
-            ach = per_cu / (dom_ms * 1e-3 * CLOCK_HZ)
-            issue = {"bound": "VALU+SALU issue", "kernel": dom, "achieved": round(ach, 3), "peak": ISSUE_PEAK,
-                     "unit": "instructions/cycle/CU", "frac": round(ach / ISSUE_PEAK, 3),
-                     "source": "profiles/r01_pmc_summary.json (SQ_INSTS_VALU+SQ_INSTS_SALU per symbol), "
-                               "peak: scripts/micro/issue.hip"}
+    mode = "cm" if use_diff else "c"
+    roof, issue = roofline(S, N_RAW, enc_bytes, enc_ms, dec_ms, mode, args.kind)
     result = {
         "metric": METRIC, "value": round(value, 4), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": f"synthetic {args.kind} (SURVEY.md App. D, seed 0x5EED), generated in HBM",
-        "config": {"workload": f"C5 shard: {S} x 512x512 {args.kind} streams per GPU, "
-                               f"{'-c -m' if use_diff else '-c'} encode + decode round trip",
-                   "streams_per_gpu": S, "stream_bytes": N_RAW, "mode": "-c -m" if use_diff else "-c",
+        "config": {"workload": f"C5: {args.streams} x 512x512 {args.kind} streams over {world} GPU(s) "
+                               f"({S} per GPU), {'-c -m' if use_diff else '-c'} encode + decode round trip",
+                   "streams_total": args.streams, "streams_per_gpu": S, "stream_bytes": N_RAW,
+                   "mode": "-c -m" if use_diff else "-c",
                    "parallelism": f"dp{world} (stream shards, no data-path collective)"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(dom_ms, 4)},
-        "issue": issue,
+        "roofline": roof, "issue": issue,
         "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
         "encode_GiBps": round(world * S * N_RAW / (enc_ms * 1e-3) / 2**30, 4),
         "decode_GiBps": round(world * S * N_RAW / (dec_ms * 1e-3) / 2**30, 4),
         "bits_per_byte": round(enc_total * 8 / raw_total, 4), "bit_exact": True,
-        "streams_total": int(sizes.numel()),
     }
-    if gather_ms is not None:
-        result["gather_ms"] = round(gather_ms, 3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(args, cores)
+        sample = min(args.cpu_sample or 8 * cores, S)
+        cb = cpu_baseline(args, cores, [b.encoded(k) for k in range(sample)])
+        if cb is not None:
+            if not cb["bit_exact_vs_gpu"]:
+                raise SystemExit("GPU encodings differ from the reference binary's on the sampled streams")
+            result["cpu_baseline"] = cb
+            result["bit_exact_vs_reference_streams"] = sample
+    del b
+    torch.cuda.empty_cache()
+    cbad = 0
+    if world == 1 and not args.no_configs:
+        result["configs"], cbad = run_configs(torch, hc, dev, stream, set())
+        result["configs_bit_exact"] = cbad == 0
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if cbad:
+        raise SystemExit(f"config checks FAILED on {cbad} items")
 
 
 if __name__ == "__main__":

@@ -67,11 +67,16 @@ extern "C" int hc_synth_batch(int kind, uint64_t k0, uint32_t n_streams, uint64_
                               uint8_t *d_out, uint64_t stride, void *stream)
 {
     if (n_streams == 0 || width * height == 0) return HC_OK;
-    if (!d_out || kind < 0 || kind > 2 || n_streams > 65535) return HC_ERR_ARG;
+    if (!d_out || kind < 0 || kind > 2) return HC_ERR_ARG;
     const uint64_t n = width * height;
     uint64_t blocks = (n / 4 + 255) / 256;
     if (blocks > 1024) blocks = 1024;
-    synth_kernel<<<dim3((unsigned)blocks, n_streams), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
-        kind, k0, width, height, d_out, stride);
-    return hipGetLastError() == hipSuccess ? HC_OK : HC_ERR_DEVICE;
+    // grid.y (the stream) is limited to 65535: launch in chunks
+    for (uint32_t s0 = 0; s0 < n_streams; s0 += 65535u) {
+        const uint32_t cnt = n_streams - s0 < 65535u ? n_streams - s0 : 65535u;
+        synth_kernel<<<dim3((unsigned)blocks, cnt), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
+            kind, k0 + s0, width, height, d_out + s0 * stride, stride);
+        if (hipGetLastError() != hipSuccess) return HC_ERR_DEVICE;
+    }
+    return HC_OK;
 }

@@ -133,10 +133,34 @@ def _dp(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status):
+    """The batch entry points take raw device pointers: a CPU, non-contiguous or wrongly typed
+    tensor would become an out-of-bounds device access, so reject it here instead."""
+    import torch
+    n = in_offs.numel()
+    spec = (("in", inp, torch.uint8, None), ("in_offs", in_offs, torch.int64, n),
+            ("in_lens", in_lens, torch.int64, n), ("out", out, torch.uint8, None),
+            ("out_offs", out_offs, torch.int64, n), ("out_caps", out_caps, torch.int64, n),
+            ("out_lens", out_lens, torch.int64, n), ("status", status, torch.int32, n))
+    dev = inp.device
+    for name, t, dt, numel in spec:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name}: expected a torch tensor")
+        if not t.is_cuda or t.device != dev:
+            raise ValueError(f"{name}: expected a CUDA tensor on {dev}, got {t.device}")
+        if t.dtype != dt:
+            raise TypeError(f"{name}: expected {dt}, got {t.dtype}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name}: not contiguous")
+        if numel is not None and t.numel() != numel:
+            raise ValueError(f"{name}: {t.numel()} entries for {n} streams")
+    return n
+
+
 def compress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status,
                    use_diff=False, stream=None):
     """hc_compress_batch on torch CUDA tensors (uint8 data, int64 offsets/lengths, int32 status)."""
-    n = in_offs.numel()
+    n = _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status)
     rc = lib().hc_compress_batch(_dp(inp), _dp(in_offs), _dp(in_lens), n,
                                  HC_FLAG_DIFF if use_diff else 0, _dp(out), _dp(out_offs),
                                  _dp(out_caps), _dp(out_lens), _dp(status), _stream_handle(stream))
@@ -145,7 +169,8 @@ def compress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, sta
 
 
 def decompress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status, stream=None):
-    n = in_offs.numel()
+    """hc_decompress_batch on torch CUDA tensors (same layout as compress_batch)."""
+    n = _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status)
     rc = lib().hc_decompress_batch(_dp(inp), _dp(in_offs), _dp(in_lens), n, _dp(out),
                                    _dp(out_offs), _dp(out_caps), _dp(out_lens), _dp(status),
                                    _stream_handle(stream))
