@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--no-diff", action="store_true", help="-c instead of -c -m")
     ap.add_argument("--cpu-sample", type=int, default=0, help="streams for the CPU baseline (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="after the timed region: pack every rank's encoded shard on its GPU and send it to rank 0 "
+                         "(the north star's final gather), timed and reported separately")
     ap.add_argument("--no-configs", action="store_true", help="N=1: skip the other BASELINE configs")
     ap.add_argument("--only-configs", default="", help="comma list: run just these configs (no headline)")
     return ap.parse_args()
@@ -299,6 +302,32 @@ def run_configs(torch, hc, dev, stream, only):
     return res, bad
 
 
+def time_gather(torch, hcdist, b, dev, barrier):
+    """every rank's encoded streams packed back to back on its GPU (hc_pack_batch), then sent to
+    rank 0 point to point; max over ranks of the wall time; rank 0 checks the bytes it got"""
+    ms = []
+    for _ in range(2):
+        if barrier:
+            barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        packed, sizes = hcdist.gather_encoded(b.enc, b.eoffs, b.elens)
+        torch.cuda.synchronize(dev)
+        if barrier:
+            barrier()
+        ms.append((time.perf_counter() - t0) * 1e3)
+    ms = float(hcdist.reduce_counters([min(ms)], op="max", device=dev)[0])
+    total = int(sizes.sum())
+    out = {"bytes_to_rank0": total, "ms": round(ms, 3), "GBps": round(total / (ms * 1e-3) / 1e9, 2),
+           "how": "hc_pack_batch on each GPU, then batch_isend_irecv to rank 0 (RCCL p2p over xGMI)"}
+    if packed is not None:
+        k = b.S - 1  # rank 0's own last stream sits at the end of its shard in the packed buffer
+        at = int(b.elens[:k].sum())
+        out["rank0_spot_check"] = bool(torch.equal(packed[at:at + int(b.elens[k])],
+                                                   b.enc[int(b.eoffs[k]):int(b.eoffs[k]) + int(b.elens[k])]))
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -359,6 +388,8 @@ def main():
         "decode_GiBps": round(world * S * N_RAW / (dec_ms * 1e-3) / 2**30, 4),
         "bits_per_byte": round(enc_total * 8 / raw_total, 4), "bit_exact": True,
     }
+    if args.gather:
+        result["gather"] = time_gather(torch, hcdist, b, dev, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = min(16, os.cpu_count() or 1)
         sample = min(args.cpu_sample or 8 * cores, S)

@@ -33,15 +33,31 @@ __global__ void kept_lengths(const uint64_t *lens, const int32_t *status, uint64
     if (i < n) kept[i] = status[i] == 0 ? lens[i] : 0;
 }
 
-// stream i's kept bytes from out + offs[i] to packed + at[i]; one workgroup per stream
-__global__ __launch_bounds__(256) void compact(const uint8_t *out, const uint64_t *offs, const uint64_t *kept,
-                                               const uint64_t *at, uint8_t *packed)
+// stream i's len[i] bytes from src + soffs[i] to dst + doffs[i]; one workgroup per stream per
+// grid-stride step. The destination is packed back to back (any byte alignment): a byte head
+// up to the next 16-byte boundary, then 16-byte aligned stores fed by unaligned 16-byte loads
+// (global_load_dwordx4 takes any address on gfx950), then a byte tail.
+typedef uint4 uint4_u __attribute__((aligned(1)));
+__global__ __launch_bounds__(256) void pack_kernel(const uint8_t *src, const uint64_t *soffs, const uint64_t *lens,
+                                                   uint32_t n, uint8_t *dst, const uint64_t *doffs)
 {
-    const uint32_t i = blockIdx.x;
-    const uint8_t *src = out + offs[i];
-    uint8_t *dst = packed + at[i];
-    const uint64_t len = kept[i];
-    for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) dst[k] = src[k];
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint8_t *s = src + soffs[i];
+        uint8_t *d = dst + doffs[i];
+        const uint64_t len = lens[i];
+        uint64_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
+        if (head > len) head = len;
+        if (threadIdx.x < head) d[threadIdx.x] = s[threadIdx.x];
+        const uint64_t body = (len - head) / 16;
+        const uint4_u *s16 = reinterpret_cast<const uint4_u *>(s + head);
+        uint4 *d16 = reinterpret_cast<uint4 *>(d + head);
+        for (uint64_t k = threadIdx.x; k < body; k += blockDim.x) {
+            const uint4 v = {s16[k].x, s16[k].y, s16[k].z, s16[k].w};
+            d16[k] = v;
+        }
+        const uint64_t t0 = head + body * 16;
+        if (t0 + threadIdx.x < len) d[t0 + threadIdx.x] = s[t0 + threadIdx.x];
+    }
 }
 
 template <class T>
@@ -176,7 +192,7 @@ int launch(Job &j, Slot &s)
     PIPE_CK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s.dkept.p, s.dat.p, (int)n, s.st));
     PIPE_CK(s.dtmp.need(tb));
     PIPE_CK(hipcub::DeviceScan::ExclusiveSum(s.dtmp.p, tb, s.dkept.p, s.dat.p, (int)n, s.st));
-    compact<<<n, 256, 0, s.st>>>(s.dout.p, d + 2 * n, s.dkept.p, s.dat.p, s.dpacked.p);
+    pack_kernel<<<n < 65535 ? n : 65535, 256, 0, s.st>>>(s.dout.p, d + 2 * n, s.dkept.p, n, s.dpacked.p, s.dat.p);
     PIPE_CK(hipGetLastError());
     PIPE_CK(hipMemcpyAsync(s.hdown.p, s.dlens.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s.st));
     PIPE_CK(hipMemcpyAsync(s.hdown.p + n, s.dat.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s.st));
@@ -298,6 +314,16 @@ int hc_compress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, ui
     if (flags & ~HC_FLAG_DIFF) return HC_ERR_ARG;
     Job j{true, flags, in, in_lens, out, out_caps, out_lens, status, {}};
     return run(j, n_streams);
+}
+
+int hc_pack_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *lens, uint32_t n_streams,
+                  uint8_t *out, const uint64_t *out_offs, void *stream)
+{
+    if (n_streams == 0) return HC_OK;
+    if (!in || !in_offs || !lens || !out || !out_offs) return HC_ERR_ARG;
+    pack_kernel<<<n_streams < 65535 ? n_streams : 65535, 256, 0, static_cast<hipStream_t>(stream)>>>(
+        in, in_offs, lens, n_streams, out, out_offs);
+    return hipGetLastError() == hipSuccess ? HC_OK : HC_ERR_DEVICE;
 }
 
 int hc_decompress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, uint32_t n_streams,

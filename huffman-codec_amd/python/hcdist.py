@@ -34,28 +34,48 @@ def gather_sizes(lens):
 
 
 def pack(buf, offs, lens):
-    """Concatenate the byte ranges buf[offs[i]:offs[i]+lens[i]] (device gather, no host copy)."""
-    idx = torch.repeat_interleave(offs, lens) + (
-        torch.arange(int(lens.sum()), device=buf.device) -
-        torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens))
-    return buf[idx]
+    """Concatenate the byte ranges buf[offs[i]:offs[i]+lens[i]]. On the GPU this is the
+    hc_pack_batch kernel (no index tensors: 16-byte copies straight into the packed buffer);
+    CPU tensors (the gloo tests) are sliced on the host."""
+    total = int(lens.sum())
+    out = torch.empty(total, dtype=torch.uint8, device=buf.device)
+    if total == 0:
+        return out
+    dst = torch.cumsum(lens, 0) - lens
+    if buf.is_cuda:
+        import hcodec
+        hcodec.pack_batch(buf, offs.contiguous(), lens.contiguous(), out, dst.contiguous())
+    else:
+        for o, n, d in zip(offs.tolist(), lens.tolist(), dst.tolist()):
+            out[d:d + n] = buf[o:o + n]
+    return out
 
 
 def gather_encoded(buf, offs, lens):
     """Encoded streams of every rank, packed back to back in global stream order, on rank 0
-    (None elsewhere), with the all-gathered sizes. One all-gather of sizes, then one padded
-    all-gather of the packed payloads (RCCL ring over xGMI)."""
+    (None elsewhere), with the all-gathered sizes. Each rank packs its shard on the device,
+    then sends it straight to rank 0 (one point-to-point transfer per rank, all posted at once
+    by batch_isend_irecv: over xGMI every rank's shard travels on its own link to GPU 0; no
+    rank receives any payload but rank 0, and nothing is padded)."""
     packed = pack(buf, offs, lens)
     sizes = gather_sizes(lens)
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return packed, sizes
-    world = dist.get_world_size()
-    per_rank = sizes.view(world, -1).sum(1)
-    cap = int(per_rank.max())
-    pad = torch.zeros(cap, dtype=torch.uint8, device=buf.device)
-    pad[: packed.numel()] = packed
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
-    if dist.get_rank() != 0:
+    world, rank = dist.get_world_size(), dist.get_rank()
+    per_rank = sizes.view(world, -1).sum(1).tolist()
+    if rank != 0:
+        if per_rank[rank]:
+            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed, 0)]):
+                w.wait()
         return None, sizes
-    return torch.cat([p[: int(n)] for p, n in zip(parts, per_rank)]), sizes
+    out = torch.empty(sum(per_rank), dtype=torch.uint8, device=buf.device)
+    out[:per_rank[0]] = packed
+    ops, at = [], per_rank[0]
+    for r in range(1, world):
+        if per_rank[r]:
+            ops.append(dist.P2POp(dist.irecv, out[at:at + per_rank[r]], r))
+        at += per_rank[r]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return out, sizes

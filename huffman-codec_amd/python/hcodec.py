@@ -81,6 +81,7 @@ def lib():
     L.hc_decompress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
     L.hc_compress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp]
     L.hc_decompress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, vp, vp, vp, vp]
+    L.hc_pack_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp]
     L.hc_version.restype = ctypes.c_char_p
     L.hc_device_ok.restype = ctypes.c_int
     L.hc_device_info.argtypes = [ctypes.c_char_p, u64]
@@ -176,6 +177,23 @@ def decompress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, s
                                    _stream_handle(stream))
     if rc:
         raise HCodecError(f"hc_decompress_batch failed: {rc}")
+
+
+def pack_batch(inp, in_offs, lens, out, out_offs, stream=None):
+    """hc_pack_batch on CUDA tensors: out[out_offs[i]:+lens[i]] = inp[in_offs[i]:+lens[i]]."""
+    import torch
+    n = in_offs.numel()
+    for name, t, dt in (("in", inp, torch.uint8), ("in_offs", in_offs, torch.int64), ("lens", lens, torch.int64),
+                        ("out", out, torch.uint8), ("out_offs", out_offs, torch.int64)):
+        if not (isinstance(t, torch.Tensor) and t.is_cuda and t.device == inp.device and t.dtype == dt
+                and t.is_contiguous()):
+            raise ValueError(f"{name}: expected a contiguous {dt} CUDA tensor on {inp.device}")
+    if lens.numel() != n or out_offs.numel() != n:
+        raise ValueError("in_offs, lens and out_offs must have one entry per range")
+    rc = lib().hc_pack_batch(_dp(inp), _dp(in_offs), _dp(lens), n, _dp(out), _dp(out_offs),
+                             _stream_handle(stream))
+    if rc:
+        raise HCodecError(f"hc_pack_batch failed: {rc}")
 
 
 def _host_batch(fn, blobs, caps, *extra):

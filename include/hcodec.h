@@ -121,6 +121,13 @@ int hc_decompress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, 
                              uint8_t *const *out, const uint64_t *out_caps, uint64_t *out_lens,
                              int32_t *status);
 
+/* Device-side packing of many byte ranges into one buffer (e.g. a batch's encoded streams,
+ * back to back, before they leave the GPU or cross to rank 0): copies lens[i] bytes from
+ * in + in_offs[i] to out + out_offs[i] for every i. Asynchronous on `stream`; ranges must not
+ * overlap. No reference counterpart (the reference writes one file per process). */
+int hc_pack_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *lens, uint32_t n_streams,
+                  uint8_t *out, const uint64_t *out_offs, void *stream);
+
 /* Library version string and a device check (1 = a gfx950 device is usable). */
 const char *hc_version(void);
 int hc_device_ok(void);

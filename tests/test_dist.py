@@ -49,14 +49,18 @@ def _worker(rank, world, port, q):
     buf, offs, lens = _encode_shard(rank, world)
     total = hcdist.reduce_counters([int(lens.sum()), rank + 1])
     mx = hcdist.reduce_counters([float(rank)], op="max")
+    own = hcdist.pack(buf, offs, lens)
     packed, sizes = hcdist.gather_encoded(buf, offs, lens)
-    q.put((rank, total.tolist(), mx.tolist(), sizes.tolist(), None if packed is None else packed.numpy().tobytes()))
+    q.put((rank, total.tolist(), mx.tolist(), sizes.tolist(), None if packed is None else packed.numpy().tobytes(),
+           own.numel()))
     dist.destroy_process_group()
 
 
-def test_two_rank_gather_matches_single_process(oracle_mod):
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_rank_gather_matches_single_process(oracle_mod, world):
+    """rank 0 receives every rank's shard (point to point, in stream order); the other ranks
+    receive nothing and hold only their own packed shard (no padding to the largest rank)"""
     import hcdist
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -75,11 +79,13 @@ def test_two_rank_gather_matches_single_process(oracle_mod):
     for k in range(world * PER_RANK):
         want.append(oracle_mod.compress(oracle_mod.synth("photo", k, W, H).tobytes(), True, False, 512)[1])
     for r in range(world):
-        assert res[r][1] == [sum(map(len, want)), 3]
-        assert res[r][2] == [1.0]
+        assert res[r][1] == [sum(map(len, want)), world * (world + 1) // 2]
+        assert res[r][2] == [float(world - 1)]
         assert res[r][3] == [len(b) for b in want]
+        assert res[r][5] == sum(len(b) for b in want[r * PER_RANK:(r + 1) * PER_RANK])
+        if r:
+            assert res[r][4] is None
     assert res[0][4] == b"".join(want)
-    assert res[1][4] is None
     assert list(hcdist.shard(1, 2, 3)) == [3, 4, 5]
 
 
