@@ -1,0 +1,239 @@
+"""Executable model of the adaptive-RLE kernels' arithmetic (huffman-codec_amd/csrc/hc_adapt.hip),
+checked against the oracle by tests/test_adapt_model.py. Pure Python on small matrices.
+
+Block cost (transform.cpp:97-134 measures |applyRLE(block scan)|, transform.cpp:241-279) is
+computed WITHOUT emitting: the scan of a block is a bit string e (bit p = element p equals
+element p-1; bit 0 forced to 0 at the block start), and the MNP-5 length is a function of its
+maximal runs: every run but the last costs run_cost(L), the last
+run_cost(L-1)+1. A bit string segment folds into Seg(n, lead, tail, mid):
+  lead = ones before the first zero (they extend the run of the previous segment; = n if none),
+  tail = ones after the last zero, mid = cost of the runs that start and end inside.
+Segments join associatively (seg_join); a leaf is one <= 64-bit word (seg_leaf), where every
+run strictly inside the word is < 64 long and so costs g(L) = 1, 2, 4 for L = 1, 2, >= 3: a
+pattern count of the word's bits. The kernels build the words from per-tile "equal to the left
+neighbour" / "equal to the upper neighbour" bit rows (Eh, Ev), substituting the first bit of
+every block row / column with the comparison the block scan makes across the row wrap.
+"""
+
+
+def run_cost(L):
+    q, r = divmod(L, 258)
+    return 4 * q + (0 if r == 0 else (r if r < 3 else 4))
+
+
+def popc(x):
+    return bin(x).count("1")
+
+
+M64 = (1 << 64) - 1
+
+
+class Seg:
+    __slots__ = ("n", "lead", "tail", "mid")
+
+    def __init__(self, n=0, lead=0, tail=0, mid=0):
+        self.n, self.lead, self.tail, self.mid = n, lead, tail, mid
+
+    def __repr__(self):
+        return f"Seg(n={self.n}, lead={self.lead}, tail={self.tail}, mid={self.mid})"
+
+
+def seg_leaf(w, n):
+    """bits 0..n-1 of w (bit i = element i equals its predecessor), 1 <= n <= 64"""
+    valid = M64 if n == 64 else (1 << n) - 1
+    w &= valid
+    z = ~w & valid
+    if z == 0:
+        return Seg(n, n, 0, 0)
+    f = (z & -z).bit_length() - 1
+    l = z.bit_length() - 1
+    m = ((1 << l) - 1) & ~((1 << f) - 1)
+    mid = popc(z & m) + popc(w & (z << 1) & m) + 2 * popc(w & (w << 1) & (z << 2) & m)
+    return Seg(n, f, n - 1 - l, mid)
+
+
+def seg_join(x, y):
+    x0, y0 = x.lead < x.n, y.lead < y.n
+    if not y0:
+        return Seg(x.n + y.n, x.lead if x0 else x.n + y.n, x.tail + y.n if x0 else 0, x.mid)
+    if not x0:
+        return Seg(x.n + y.n, x.n + y.lead, y.tail, y.mid)
+    return Seg(x.n + y.n, x.lead, y.tail, x.mid + run_cost(x.tail + 1 + y.lead) + y.mid)
+
+
+def seg_cost(s):
+    """cost of a whole block scan whose first bit is 0"""
+    assert s.n == 0 or s.lead == 0
+    return 0 if s.n == 0 else s.mid + run_cost(s.tail) + 1
+
+
+def bits_of(seq):
+    """reference-side helper: the e bit string of a sequence (bit 0 = 0)"""
+    return [0] + [int(seq[i] == seq[i - 1]) for i in range(1, len(seq))]
+
+
+def fold_bits(bits):
+    """fold a bit list through 64-bit leaves and joins (any chunking gives the same result)"""
+    s = Seg()
+    for k in range(0, len(bits), 64):
+        chunk = bits[k:k + 64]
+        w = sum(b << i for i, b in enumerate(chunk))
+        s = seg_join(s, seg_leaf(w, len(chunk)))
+    return s
+
+
+def rle_len_via_bits(seq):
+    return seg_cost(fold_bits(bits_of(seq)))
+
+
+# --------------------------------------------------------------------------- tile model ---
+
+TILE = 128
+
+
+def diffed(m, use_diff):
+    """the linear diff model (transform.cpp:220-229) as the kernels see it: D[i] = m[i] - m[i-1]"""
+    if not use_diff:
+        return list(m)
+    return [(m[i] - (m[i - 1] if i else 0)) & 255 for i in range(len(m))]
+
+
+def block_geo(W, H, B, i):
+    per_row = -(-W // B)
+    x0, y0 = (i % per_row) * B, (i // per_row) * B
+    return x0, y0, min(B, W - x0), min(B, H - y0)
+
+
+def block_costs_tiled(m, W, H, B, use_diff=False):
+    """(h, v) cost of every block at block size B <= 128, computed the way tile_cost_kernel
+    does: per 128x128 tile, Eh rows / Ev columns as two 64-bit words, one row piece (h) or column
+    piece (v) per lane with its first bit substituted, leaves joined in scan order."""
+    D = diffed(m, use_diff)
+    at = lambda x, y: D[y * W + x]
+    nb = (-(-W // B)) * (-(-H // B))
+    out = [None] * nb
+    for ty0 in range(0, H, TILE):
+        for tx0 in range(0, W, TILE):
+            tw, th = min(TILE, W - tx0), min(TILE, H - ty0)
+            Eh = [[0, 0] for _ in range(th)]
+            Ev = [[0, 0] for _ in range(tw)]
+            for r in range(th):
+                for c in range(tw):
+                    x, y = tx0 + c, ty0 + r
+                    if x > 0 and at(x, y) == at(x - 1, y):
+                        Eh[r][c >> 6] |= 1 << (c & 63)
+                    if y > 0 and at(x, y) == at(x, y - 1):
+                        Ev[c][r >> 6] |= 1 << (r & 63)
+            for by in range(-(-th // B)):
+                for bx in range(-(-tw // B)):
+                    x0, y0 = tx0 + bx * B, ty0 + by * B
+                    sx, sy = min(B, W - x0), min(B, H - y0)
+                    i = (y0 // B) * (-(-W // B)) + x0 // B
+                    h = Seg()
+                    for r in range(sy):
+                        y = y0 + r
+                        rs = 0 if r == 0 else int(at(x0, y) == at(x0 + sx - 1, y - 1))
+                        h = seg_join(h, piece(Eh[y - ty0], x0 - tx0, sx, rs))
+                    v = Seg()
+                    for c in range(sx):
+                        x = x0 + c
+                        cs = 0 if c == 0 else int(at(x, y0) == at(x - 1, y0 + sy - 1))
+                        v = seg_join(v, piece(Ev[x - tx0], y0 - ty0, sy, cs))
+                    out[i] = (seg_cost(h), seg_cost(v))
+    return out
+
+
+def piece(words, off, n, first):
+    """bits [off, off + n) of a 128-bit row (two words), bit 0 replaced by `first`"""
+    full = words[0] | (words[1] << 64)
+    bits = (full >> off) & ((1 << n) - 1)
+    bits = (bits & ~1) | first
+    s = Seg()
+    for k in range(0, n, 64):
+        s = seg_join(s, seg_leaf((bits >> k) & M64, min(64, n - k)))
+    return s
+
+
+def tile_pieces(m, W, H, use_diff=False):
+    """what tile_cost_kernel writes for the blocks larger than a tile: per tile row its h piece
+    (summary of bits 1..tw-1, bit 0 = Eh at the tile's first column, first and last value), per
+    tile column its v piece. Keyed (y, tix) / (x, tiy)."""
+    D = diffed(m, use_diff)
+    at = lambda x, y: D[y * W + x]
+    hp, vp = {}, {}
+    for ty0 in range(0, H, TILE):
+        for tx0 in range(0, W, TILE):
+            tw, th = min(TILE, W - tx0), min(TILE, H - ty0)
+            for r in range(th):
+                y = ty0 + r
+                bits = [int(x > 0 and at(x, y) == at(x - 1, y)) for x in range(tx0, tx0 + tw)]
+                hp[(y, tx0 // TILE)] = (fold_bits(bits[1:]) if tw > 1 else Seg(), bits[0], at(tx0, y),
+                                        at(tx0 + tw - 1, y), tw)
+            for c in range(tw):
+                x = tx0 + c
+                bits = [int(y > 0 and at(x, y) == at(x, y - 1)) for y in range(ty0, ty0 + th)]
+                vp[(x, ty0 // TILE)] = (fold_bits(bits[1:]) if th > 1 else Seg(), bits[0], at(x, ty0),
+                                        at(x, ty0 + th - 1), th)
+    return hp, vp
+
+
+def big_block_cost(hp, vp, W, H, B, i):
+    """cost_big_kernel: the (h, v) cost of block i (B >= 256) from the tile pieces"""
+    x0, y0, sx, sy = block_geo(W, H, B, i)
+    h = Seg()
+    prev_last = None
+    for r in range(sy):
+        y = y0 + r
+        row = Seg()
+        for t in range(x0 // TILE, (x0 + sx - 1) // TILE + 1):
+            s, e0, first, last, n = hp[(y, t)]
+            b0 = (0 if r == 0 else int(first == prev_last)) if t == x0 // TILE else e0
+            row = seg_join(row, seg_join(seg_leaf(b0, 1), s))
+            lastv = last
+        prev_last = lastv
+        h = seg_join(h, row)
+    v = Seg()
+    prev_last = None
+    for c in range(sx):
+        x = x0 + c
+        col = Seg()
+        for t in range(y0 // TILE, (y0 + sy - 1) // TILE + 1):
+            s, e0, first, last, n = vp[(x, t)]
+            b0 = (0 if c == 0 else int(first == prev_last)) if t == y0 // TILE else e0
+            col = seg_join(col, seg_join(seg_leaf(b0, 1), s))
+            lastv = last
+        prev_last = lastv
+        v = seg_join(v, col)
+    return seg_cost(h), seg_cost(v)
+
+
+# --------------------------------------------------------------------------- emit model ---
+
+def emit_lanes(seq):
+    """emit_kernel's per-position rule (64 elements per step, run offset carried): element p of
+    a block scan emits 0, 1 or 2 bytes from its offset o in its run (j = o mod 258) and whether
+    its run ends there; the last element is always one literal (transform.cpp:252)."""
+    n = len(seq)
+    out = []
+    o = 0
+    for p in range(n):
+        o = 0 if p == 0 or seq[p] != seq[p - 1] else o + 1
+        v = seq[p]
+        if p == n - 1:
+            out.append(v)
+            continue
+        j = o % 258
+        end = p == n - 2 or seq[p + 1] != v
+        if j <= 2:
+            out.append(v)
+        elif j == 257:
+            out.append(255)
+        if end and 2 <= j <= 256:
+            out.append(j - 2)
+    return out
+
+
+def scan(m, W, x0, y0, sx, sy, horiz):
+    if horiz:
+        return [m[(y0 + r) * W + x0 + c] for r in range(sy) for c in range(sx)]
+    return [m[(y0 + r) * W + x0 + c] for c in range(sx) for r in range(sy)]
