@@ -1,270 +1,859 @@
-// hc_adapt.hip — adaptive block RLE (encode search + emit, decode) and the diff model on gfx950.
+// hc_adapt.hip — adaptive block RLE on gfx950, batched: many W x H matrices per call.
 //
-// Reference: transform.cpp:294-328 (block-size search), transform.cpp:97-134 (per-block
-// horizontal / vertical choice), transform.cpp:66-94 + 25-62 (block scan geometry),
-// headers.cpp:18-105 (adaptive header), transform.cpp:330-361 + 162-216 (revert),
-// transform.cpp:220-239 (diff model).
+// Reference: transform.cpp:294-328 (block-size search), transform.cpp:97-134 (per-block h / v
+// choice), transform.cpp:25-94 (block geometry and scan order), headers.cpp:18-105 (adaptive
+// header), transform.cpp:330-361 + 137-216 (revert), transform.cpp:220-239 (diff model),
+// transform.cpp:241-279 (MNP-5 RLE). Model of the arithmetic: tests/adapt_cost_model.py.
 //
-// Encode: for every candidate block size B (8 .. 1024, <= W, <= H, <= 7 doublings) one
-// workgroup per (block, scan order) folds the scan into a run summary (a monoid over byte
-// runs whose closed-form MNP-5 cost, SURVEY.md Appendix A.3, gives the block's RLE length
-// without emitting it); per-block min/argmin and the candidate's total follow; the host picks
-// the first minimum; an exclusive scan of the chosen lengths places each block; one lane per
-// block then emits its RLE bytes. Decode: one wavefront finds each block's start in the symbol
-// stream (a wave scan of the revert machine's transition functions and of output lengths per
-// 256 symbols), then one lane per block reverts and scatters in parallel; the diff revert is a
-// parallel mod-256 scan.
-#include <hipcub/hipcub.hpp>
-
-#include <vector>
+// Encode (per batch, every kernel a persistent grid over a device-built work list):
+//   plan      one workgroup: validate each matrix (4 / 6 / 12), count its tiles, candidate
+//             block sizes, cost words and workspace slab; exclusive scans place everything.
+//   tile      one workgroup per 128 x 128 tile: the tile (diff model applied on the fly) is
+//             loaded once into LDS; 64-lane ballots turn it into "equal to the left / upper
+//             neighbour" bit rows (Eh, Ev); every candidate B = 8..128 then costs every block
+//             in both scan orders from those words: one block row (h) or column (v) per lane,
+//             its first bit substituted by the comparison across the scan's row wrap, folded
+//             by the run-segment monoid (no bytes emitted: the MNP-5 length is a closed form of
+//             the runs) and joined across the block's lanes in order. Per
+//             block one word (cost | h-flag) and per candidate one atomic total. For B >= 256
+//             the tile also writes one 8-byte summary per tile row / column.
+//   big       one workgroup per block of B >= 256: joins the tile summaries of its rows /
+//             columns.
+//   choose    one workgroup per matrix: first minimum of header + data over B
+//             (transform.cpp:309-325), header + direction bits, exclusive scan of the winner's
+//             block lengths in place.
+//   emit      one wave per block: MNP-5 of the block's scan, 64 elements per step, from each
+//             element's run offset (ballot of run starts, carried across steps); byte offsets
+//             by ballot popcounts.
+//   FGK       the batched FGK encoder over the symbol streams (hc_fgk.hip, SRC_SYMBOLS).
+// Decode:
+//   plan / FGK decode to symbols / parse headers (10, 11, 66, 67, capacity) / scan groups;
+//   bounds    one wave per stream: where every K-th block starts (a wave scan of the revert
+//             machine's transition functions and output lengths per 256 symbols), reporting
+//             13 / 14 / 15 where the reference exits;
+//   unblock   one wave per group of K blocks (>= 1024 bytes): revert + scatter in scan order;
+//   undiff    per 16 KB chunk: byte sums, a per-stream scan of them, byte prefix sums.
+#include <hip/hip_runtime.h>
 
 #include "hc_internal.h"
 
 namespace hc {
 namespace {
 
-// ------------------------------------------------------------------------- run summary ---
+constexpr uint32_t kTile = 128;
+constexpr uint32_t kCand = 8;        // B = 8 << c, c = 0..7 (transform.cpp:294-328, <= 7 doublings)
+constexpr uint32_t kTileCand = 5;    // B <= 128: inside one tile
+constexpr uint32_t kDS = 132;        // LDS row stride of a tile: 33 dwords, column reads conflict-free
+constexpr uint32_t kGrid = 2048;     // persistent grids: workgroups
+constexpr uint32_t kChunk = 16384;   // diff revert chunk
+constexpr uint32_t kGroupBytes = 1024;
 
-// MNP-5 bytes of a run of L equal bytes that is not the sequence's last run (closed form of
-// transform.cpp:241-279): full 258-chunks cost 4, a remainder r costs r (r < 3) or 4.
-__device__ __forceinline__ uint64_t run_cost(uint64_t L)
-{
-    const uint64_t r = L % 258;
-    return 4 * (L / 258) + (r == 0 ? 0 : (r < 3 ? r : 4));
-}
-// the last run of a sequence: its final byte is always a literal (transform.cpp:252)
-__device__ __forceinline__ uint64_t last_run_cost(uint64_t L) { return run_cost(L - 1) + 1; }
-
-struct Runs {
-    uint64_t n;    // bytes covered (0 = identity)
-    uint64_t fa;   // length of the first run
-    uint64_t lz;   // length of the last run
-    uint64_t mid;  // cost of the runs strictly between the first and the last
-    uint32_t a, z; // first and last byte
-    uint32_t single;
+struct AMeta {
+    uint64_t w, h;
+    uint64_t cost0[kCand];           // encode: first cost word of candidate c
+    unsigned long long total[kCand];  // encode: data bytes of candidate c
+    uint64_t nbc[kCand];             // encode: blocks of candidate c
+    uint64_t pieces;                 // encode: first tile-summary entry
+    uint64_t slab;                   // first byte of the stream's workspace slab
+    uint64_t sym;                    // first symbol byte (workspace offset)
+    uint64_t starts;                 // decode: first group-start entry (workspace offset, bytes)
+    uint64_t csum;                   // decode: first chunk-sum byte (workspace offset)
+    uint64_t nb, B, K, groups, chunks, hdr, count;
+    uint32_t nc, diff;
+    int32_t status;
+    uint32_t best;                   // encode: the chosen candidate
 };
 
-__device__ __forceinline__ Runs runs_empty()
+// workspace: [meta n][idx0 n+1][idx1 n+1][idx2 n+1][idx3 n+1][sym_offs n][sym_lens n][sym_caps n]
+//            [lens2 n][counters 16][slabs ...]
+struct Ws {
+    AMeta *meta;
+    uint64_t *idx[4];
+    uint64_t *sym_offs, *sym_lens, *sym_caps, *lens2;
+    unsigned long long *ctr;
+    uint8_t *base;       // the workspace itself (slab offsets are relative to it)
+    uint64_t slab0, slab_end;
+    uint32_t n;
+};
+
+__host__ __device__ inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+__host__ __device__ inline uint64_t cdiv(uint64_t a, uint64_t b) { return a / b + (a % b != 0); }
+
+uint64_t ws_header(uint32_t n)
 {
-    Runs r;
-    r.n = r.fa = r.lz = r.mid = 0;
-    r.a = r.z = 0;
-    r.single = 0;
-    return r;
+    return align_up((uint64_t)n * sizeof(AMeta), 256) + 4 * align_up(8ull * (n + 1), 256) +
+           4 * align_up(8ull * n, 256) + 256;
 }
 
-__device__ __forceinline__ void runs_push(Runs &r, uint32_t c)
+Ws carve(void *work, uint64_t bytes, uint32_t n)
 {
-    if (r.n == 0) {
-        r.a = r.z = c;
-        r.fa = r.lz = 1;
-        r.single = 1;
-        r.mid = 0;
-    } else if (c == r.z) {
-        ++r.lz;
-        if (r.single) ++r.fa;
-    } else {
-        if (!r.single) r.mid += run_cost(r.lz);
-        r.single = 0;
-        r.z = c;
-        r.lz = 1;
+    Ws w;
+    uint8_t *p = static_cast<uint8_t *>(work);
+    uint64_t o = 0;
+    w.base = p;
+    w.n = n;
+    w.meta = reinterpret_cast<AMeta *>(p + o);
+    o += align_up((uint64_t)n * sizeof(AMeta), 256);
+    for (int k = 0; k < 4; ++k) {
+        w.idx[k] = reinterpret_cast<uint64_t *>(p + o);
+        o += align_up(8ull * (n + 1), 256);
     }
-    ++r.n;
+    uint64_t **arr[4] = {&w.sym_offs, &w.sym_lens, &w.sym_caps, &w.lens2};
+    for (int k = 0; k < 4; ++k) {
+        *arr[k] = reinterpret_cast<uint64_t *>(p + o);
+        o += align_up(8ull * n, 256);
+    }
+    w.ctr = reinterpret_cast<unsigned long long *>(p + o);
+    o += 256;
+    w.slab0 = o;
+    w.slab_end = bytes;
+    return w;
 }
 
-__device__ __forceinline__ Runs runs_join(const Runs &x, const Runs &y)
+// --------------------------------------------------------------------- wave / WG helpers ---
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t lanes_below(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// index i with pre[i] <= t < pre[i + 1] (pre[0] = 0, pre[n] = total, t < total)
+__device__ __forceinline__ uint32_t find_item(const uint64_t *pre, uint32_t n, uint64_t t)
 {
-    if (x.n == 0) return y;
-    if (y.n == 0) return x;
-    Runs r;
+    uint32_t lo = 0, hi = n;  // pre[lo] <= t < pre[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Exclusive scans of kC columns over n items in ONE workgroup of 1024 threads. need(i, v) fills
+// the item's values; put(i, base) receives its exclusive prefix; tot[] the totals.
+template <int kC, class Need, class Put>
+__device__ void wg_scan(uint32_t n, Need need, Put put, uint64_t *tot)
+{
+    __shared__ uint64_t part[1024][kC];
+    const uint32_t t = threadIdx.x, per = (n + 1023) / 1024;
+    const uint32_t b = t * per, e = b + per < n ? b + per : n;
+    uint64_t s[kC];
+    for (int c = 0; c < kC; ++c) s[c] = 0;
+    for (uint32_t i = b; i < e; ++i) {
+        uint64_t v[kC];
+        need(i, v);
+        for (int c = 0; c < kC; ++c) s[c] += v[c];
+    }
+    for (int c = 0; c < kC; ++c) part[t][c] = s[c];
+    __syncthreads();
+    if (t < kC) {  // one thread per column: sequential scan of 1024 partials
+        uint64_t acc = 0;
+        for (uint32_t k = 0; k < 1024; ++k) {
+            const uint64_t v = part[k][t];
+            part[k][t] = acc;
+            acc += v;
+        }
+        tot[t] = acc;
+    }
+    __syncthreads();
+    for (int c = 0; c < kC; ++c) s[c] = part[t][c];
+    for (uint32_t i = b; i < e; ++i) {
+        uint64_t v[kC];
+        need(i, v);
+        put(i, s);
+        for (int c = 0; c < kC; ++c) s[c] += v[c];
+    }
+    __syncthreads();
+}
+
+// --------------------------------------------------------------- run-segment monoid ---
+// A stretch of a block scan as a bit string (bit p = element p equals element p - 1):
+// lead = ones before the first zero (= n if none), tail = ones after the last zero, mid = MNP-5
+// bytes of the runs that start and end inside. tests/adapt_cost_model.py: Seg.
+
+struct Seg {
+    uint32_t n, lead, tail, mid;
+};
+
+__device__ __forceinline__ Seg seg_id()
+{
+    Seg s;
+    s.n = s.lead = s.tail = s.mid = 0;
+    return s;
+}
+
+// MNP-5 bytes of a run of L that is not the scan's last (closed form of transform.cpp:241-279)
+__device__ __forceinline__ uint32_t run_cost(uint32_t L)
+{
+    const uint32_t q = L / 258u, r = L - q * 258u;
+    return 4 * q + (r == 0 ? 0u : (r < 3 ? r : 4u));
+}
+
+// bits 0..n-1 of w, 1 <= n <= 64: every run strictly inside the word is < 64 long, so it
+// costs 1, 2 or 4: a pattern count of zeros, 01 and 011 (read upwards)
+__device__ __forceinline__ Seg seg_leaf(uint64_t w, uint32_t n)
+{
+    const uint64_t valid = n >= 64 ? ~0ull : ((1ull << n) - 1);
+    w &= valid;
+    const uint64_t z = ~w & valid;
+    const uint32_t f = z ? (uint32_t)__builtin_ctzll(z) : 0u;
+    const uint32_t l = z ? 63u - (uint32_t)__builtin_clzll(z) : 0u;
+    const uint64_t m = ((1ull << l) - 1) & ~((1ull << f) - 1);
+    Seg s;
+    s.n = n;
+    s.lead = z ? f : n;
+    s.tail = z ? n - 1 - l : 0u;
+    s.mid = __popcll(z & m) + __popcll(w & (z << 1) & m) + 2 * __popcll(w & (w << 1) & (z << 2) & m);
+    return s;
+}
+
+__device__ __forceinline__ Seg seg_join(const Seg &x, const Seg &y)
+{
+    const bool x0 = x.lead < x.n, y0 = y.lead < y.n;
+    Seg r;
     r.n = x.n + y.n;
-    r.a = x.a;
-    r.z = y.z;
-    if (x.z == y.a) {
-        const uint64_t m = x.lz + y.fa;
-        if (x.single && y.single) {
-            r.single = 1;
-            r.fa = r.lz = m;
-            r.mid = 0;
-        } else if (x.single) {
-            r.single = 0;
-            r.fa = m;
-            r.lz = y.lz;
-            r.mid = y.mid;
-        } else if (y.single) {
-            r.single = 0;
-            r.fa = x.fa;
-            r.lz = m;
-            r.mid = x.mid;
-        } else {
-            r.single = 0;
-            r.fa = x.fa;
-            r.lz = y.lz;
-            r.mid = x.mid + run_cost(m) + y.mid;
-        }
+    if (!y0) {
+        r.lead = x0 ? x.lead : x.n + y.n;
+        r.tail = x0 ? x.tail + y.n : 0u;
+        r.mid = x.mid;
+    } else if (!x0) {
+        r.lead = x.n + y.lead;
+        r.tail = y.tail;
+        r.mid = y.mid;
     } else {
-        r.single = 0;
-        r.fa = x.fa;
-        r.lz = y.lz;
-        r.mid = (x.single ? 0 : x.mid + run_cost(x.lz)) + (y.single ? 0 : run_cost(y.fa) + y.mid);
+        r.lead = x.lead;
+        r.tail = y.tail;
+        r.mid = x.mid + run_cost(x.tail + 1 + y.lead) + y.mid;
     }
     return r;
 }
 
-__device__ __forceinline__ uint64_t runs_total(const Runs &r)
+// cost of a whole block scan (its first bit is 0: the block starts a run)
+__device__ __forceinline__ uint32_t seg_cost(const Seg &s) { return s.n ? s.mid + run_cost(s.tail) + 1 : 0u; }
+
+__device__ __forceinline__ Seg seg_shfl_down(const Seg &s, uint32_t d)
 {
-    if (r.n == 0) return 0;
-    return r.single ? last_run_cost(r.fa) : run_cost(r.fa) + r.mid + last_run_cost(r.lz);
+    Seg r;
+    r.n = __shfl_down(s.n, d, 64);
+    r.lead = __shfl_down(s.lead, d, 64);
+    r.tail = __shfl_down(s.tail, d, 64);
+    r.mid = __shfl_down(s.mid, d, 64);
+    return r;
 }
 
-// transform.cpp:25-62
-struct Geo {
-    uint64_t x0, y0, sx, sy;
+// ordered join over aligned groups of g lanes (g a power of two <= 64); lane 0 of a group ends
+// with the group's fold
+__device__ __forceinline__ Seg seg_group(Seg s, uint32_t g, uint32_t lane)
+{
+    for (uint32_t st = 1; st < g; st <<= 1) {
+        const Seg t = seg_shfl_down(s, st);
+        if ((lane & (2 * st - 1)) == 0) s = seg_join(s, t);
+    }
+    return s;
+}
+
+// a block row / column: bits [off, off + n) of a 128-bit tile row, bit 0 replaced by `first`
+__device__ __forceinline__ Seg seg_piece(const uint64_t *w, uint32_t off, uint32_t n, uint32_t first)
+{
+    if (n <= 64) {
+        const uint64_t v = ((w[off >> 6] >> (off & 63)) & ~1ull) | first;
+        return seg_leaf(v, n);
+    }
+    return seg_join(seg_leaf((w[0] & ~1ull) | first, 64), seg_leaf(w[1], n - 64));
+}
+
+// 8-byte tile summary of a tile row / column for the blocks of B >= 256: the segment of bits
+// 1..len-1 (lead, tail: <= 127; mid <= 170), bit 0, the first and the last value
+__device__ __forceinline__ uint64_t piece_pack(const Seg &s, uint32_t e0, uint32_t first, uint32_t last)
+{
+    return (uint64_t)s.lead | (uint64_t)s.tail << 8 | (uint64_t)s.mid << 16 | (uint64_t)first << 32 |
+           (uint64_t)last << 40 | (uint64_t)e0 << 48;
+}
+__device__ __forceinline__ Seg piece_seg(uint64_t p, uint32_t n)
+{
+    Seg s;
+    s.n = n;
+    s.lead = p & 0xFF;
+    s.tail = (p >> 8) & 0xFF;
+    s.mid = (p >> 16) & 0xFFFF;
+    return s;
+}
+
+// --------------------------------------------------------------------------- encode ------
+
+struct EncArgs {
+    const uint8_t *in;
+    const uint64_t *in_offs, *in_lens, *widths;
+    uint32_t n, diff;
 };
-__device__ __forceinline__ Geo block_geo(uint64_t w, uint64_t h, uint64_t b, uint64_t i)
+
+// blocks of size b in a w x h matrix (transform.cpp:410-418)
+__host__ __device__ inline uint64_t nblocks(uint64_t w, uint64_t h, uint64_t b) { return cdiv(w, b) * cdiv(h, b); }
+
+__global__ __launch_bounds__(1024) void enc_plan_kernel(EncArgs a, Ws ws)
 {
-    const uint64_t per_row = (w + b - 1) / b;
-    Geo g;
-    g.x0 = (i % per_row) * b;
-    g.y0 = (i / per_row) * b;
-    g.sx = g.x0 + b > w ? w - g.x0 : b;
-    g.sy = g.y0 + b > h ? h - g.y0 : b;
-    return g;
+    auto need = [&](uint32_t i, uint64_t *v) {
+        const uint64_t len = a.in_lens[i], w = a.widths[i];
+        const uint64_t h = w ? len / w : 0;
+        const bool ok = w != 0 && len % w == 0 && w >= 8 && h >= 8;
+        uint64_t cost = 0, big = 0;
+        uint32_t nc = 0;
+        for (uint64_t b = 8, c = 0; ok && c < kCand && b <= w && b <= h; ++c, b *= 2, ++nc) {
+            cost += nblocks(w, h, b);
+            if (c >= kTileCand) big += nblocks(w, h, b);
+        }
+        const uint64_t ntx = cdiv(w, kTile), nty = cdiv(h, kTile);
+        const uint64_t pieces = (ok && nc > kTileCand) ? h * ntx + w * nty : 0;
+        const uint64_t nb8 = ok ? nblocks(w, h, 8) : 0;
+        // MNP-5 of a block of L bytes <= 4L/3 + 1, header 24 + one bit per block
+        const uint64_t syms = ok ? len + len / 3 + nb8 + nb8 / 8 + 64 : 0;
+        v[0] = ok ? ntx * nty : 0;
+        v[1] = big;
+        v[2] = nb8;
+        v[3] = ok ? align_up(4 * cost, 16) + align_up(8 * pieces, 16) + align_up(syms, 16) : 0;
+    };
+    auto put = [&](uint32_t i, const uint64_t *base) {
+        uint64_t v[4];
+        need(i, v);
+        AMeta &m = ws.meta[i];
+        const uint64_t len = a.in_lens[i], w = a.widths[i];
+        const uint64_t h = w ? len / w : 0;
+        m.w = w;
+        m.h = h;
+        m.diff = a.diff;
+        // main.cpp:195-199 (width 0), main.cpp:54-58 (size not a multiple of the width),
+        // transform.cpp:300-304 (either side < 8)
+        m.status = w == 0 ? HC_ERR_WIDTH : (len % w ? HC_ERR_MATRIX_SIZE : (w < 8 || h < 8 ? HC_ERR_DIMS : 0));
+        m.slab = ws.slab0 + base[3];
+        if (m.status == 0 && m.slab + v[3] > ws.slab_end) m.status = HC_ERR_CAPACITY;
+        uint64_t o = m.slab, nc = 0;
+        for (uint64_t b = 8, c = 0; c < kCand; ++c, b *= 2) {
+            m.total[c] = 0;
+            const bool on = m.status == 0 && b <= w && b <= h;
+            m.nbc[c] = on ? nblocks(w, h, b) : 0;
+            m.cost0[c] = o;  // a byte offset into the workspace
+            o += 4 * m.nbc[c];
+            nc += on;
+        }
+        m.nc = (uint32_t)nc;
+        o = align_up(o, 16);
+        m.pieces = o;
+        o += align_up(v[3] ? 8 * (nc > kTileCand ? h * cdiv(w, kTile) + w * cdiv(h, kTile) : 0) : 0, 16);
+        m.sym = o;
+        ws.sym_offs[i] = o;
+        ws.sym_lens[i] = 0;
+        ws.idx[0][i] = base[0];
+        ws.idx[1][i] = base[1];
+        ws.idx[2][i] = base[2];
+    };
+    __shared__ uint64_t tot[4];
+    wg_scan<4>(a.n, need, put, tot);
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 3; ++k) ws.idx[k][a.n] = tot[k];
+        ws.ctr[0] = tot[0];
+        ws.ctr[1] = tot[1];
+        ws.ctr[2] = tot[2];
+    }
 }
 
-constexpr int kCostThreads = 256;
-
-// grid (blocks, 2): y = 0 horizontal scan, y = 1 vertical scan. Each thread folds a contiguous
-// piece of the scan sequence; an ordered LDS tree joins the pieces.
-__global__ __launch_bounds__(kCostThreads) void block_cost_kernel(const uint8_t *m, uint64_t w,
-                                                                   uint64_t h, uint64_t b,
-                                                                   uint64_t *cost)
+template <class T>
+__device__ __forceinline__ T *at(const Ws &ws, uint64_t off)
 {
-    __shared__ Runs part[kCostThreads];
-    const uint64_t blk = blockIdx.x;
-    const bool horiz = blockIdx.y == 0;
-    const Geo g = block_geo(w, h, b, blk);
-    const uint64_t len = g.sx * g.sy;
-    const uint64_t per = (len + blockDim.x - 1) / blockDim.x;
-    const uint64_t beg = threadIdx.x * per;
-    const uint64_t end = beg + per < len ? beg + per : len;
-    Runs r = runs_empty();
-    if (beg < end) {
-        // transform.cpp:66-94: horizontal = row-major inside the block, vertical = column-major
-        const uint64_t inner = horiz ? g.sx : g.sy;
-        uint64_t o = beg / inner, q = beg % inner;  // outer / inner index of the scan
-        for (uint64_t k = beg; k < end; ++k) {
-            const uint64_t x = horiz ? q : o, y = horiz ? o : q;
-            runs_push(r, m[(g.y0 + y) * w + g.x0 + x]);
-            if (++q == inner) {
-                q = 0;
-                ++o;
+    return reinterpret_cast<T *>(ws.base + off);
+}
+
+__global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
+{
+    __shared__ uint8_t D[(kTile + 1) * kDS];  // row r <-> y = ty0 + r - 1, column c <-> x = tx0 + c - 1
+    __shared__ uint64_t E[4 * kTile];         // Eh[r][2] then Ev[c][2]
+    __shared__ uint32_t hv[2][256];           // candidate's block costs, h / v
+    __shared__ Seg part[4];
+    __shared__ uint32_t red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t ntiles = ws.ctr[0];
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t i = find_item(ws.idx[0], a.n, t);
+        AMeta &M = ws.meta[i];
+        if (M.status) continue;  // (uniform over the workgroup)
+        const uint64_t W = M.w, H = M.h;
+        const uint64_t ntx = cdiv(W, kTile), local = t - ws.idx[0][i];
+        const uint64_t tx0 = (local % ntx) * kTile, ty0 = (local / ntx) * kTile;
+        const uint32_t tw = (uint32_t)(W - tx0 < kTile ? W - tx0 : kTile);
+        const uint32_t th = (uint32_t)(H - ty0 < kTile ? H - ty0 : kTile);
+        const uint8_t *mat = a.in + a.in_offs[i];
+        const bool diff = a.diff != 0;
+        // 1. the tile plus one row above and one column to the left, diff model applied
+        //    (transform.cpp:220-229: d[k] = m[k] - m[k-1] over the linear matrix)
+        for (uint32_t r = wv; r <= th; r += 4) {
+            if (r == 0 && ty0 == 0) continue;
+            const uint64_t y = ty0 + r - 1;
+            const uint8_t *row = mat + y * W;
+            for (uint32_t c = lane; c <= tw; c += 64) {
+                if (c == 0 && tx0 == 0) continue;
+                const uint64_t x = tx0 + c - 1;
+                uint32_t v = row[x];
+                if (diff) v -= (x | y) ? row[(int64_t)x - 1] : 0u;
+                D[r * kDS + c] = (uint8_t)v;
             }
         }
-    }
-    part[threadIdx.x] = r;
-    __syncthreads();
-    for (unsigned s = 1; s < blockDim.x; s *= 2) {
-        if ((threadIdx.x % (2 * s)) == 0 && threadIdx.x + s < blockDim.x)
-            part[threadIdx.x] = runs_join(part[threadIdx.x], part[threadIdx.x + s]);
         __syncthreads();
-    }
-    if (threadIdx.x == 0) cost[blk * 2 + (horiz ? 0 : 1)] = runs_total(part[0]);
-}
-
-// transform.cpp:113-123: per block keep the shorter scan (tie -> horizontal); sum the data
-__global__ void choose_kernel(const uint64_t *cost, uint64_t nb, uint64_t *len, uint8_t *dir,
-                              unsigned long long *total)
-{
-    __shared__ unsigned long long acc[256];
-    uint64_t sum = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nb;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t lh = cost[2 * i], lv = cost[2 * i + 1];
-        const bool hz = lh <= lv;
-        len[i] = hz ? lh : lv;
-        dir[i] = hz ? 1 : 0;
-        sum += hz ? lh : lv;
-    }
-    acc[threadIdx.x] = sum;
-    __syncthreads();
-    for (unsigned s = blockDim.x / 2; s > 0; s /= 2) {
-        if (threadIdx.x < s) acc[threadIdx.x] += acc[threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) atomicAdd(total, acc[0]);
-}
-
-// headers.cpp:18-63: <u64 BE W><u64 BE H><u64 BE B><scan-direction bits, MSB first, 1 = h>
-__global__ void header_kernel(uint8_t *out, uint64_t w, uint64_t h, uint64_t b, const uint8_t *dir,
-                              uint64_t nb)
-{
-    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i < 24) {
-        const uint64_t v = i < 8 ? w : (i < 16 ? h : b);
-        out[i] = (uint8_t)(v >> (56 - 8 * (i % 8)));
-    }
-    const uint64_t nbytes = (nb + 7) / 8;
-    if (i < nbytes) {
-        uint32_t byte = 0;
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint64_t j = i * 8 + k;
-            byte = (byte << 1) | (j < nb ? dir[j] : 0u);
-        }
-        out[24 + i] = (uint8_t)byte;
-    }
-}
-
-// transform.cpp:241-279 on one block's scan, one lane per block
-__global__ void emit_kernel(const uint8_t *m, uint64_t w, uint64_t h, uint64_t b, uint64_t nb,
-                            const uint8_t *dir, const uint64_t *off, uint8_t *out)
-{
-    const uint64_t blk = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (blk >= nb) return;
-    const Geo g = block_geo(w, h, b, blk);
-    const bool horiz = dir[blk] != 0;
-    const uint64_t len = g.sx * g.sy;
-    const uint64_t inner = horiz ? g.sx : g.sy;
-    uint8_t *o = out + off[blk];
-    uint64_t p = 0, oo = 0, q = 0;
-    uint32_t run_byte = 0, run = 0;
-    for (uint64_t k = 0; k < len; ++k) {
-        const uint64_t x = horiz ? q : oo, y = horiz ? oo : q;
-        const uint32_t c = m[(g.y0 + y) * w + g.x0 + x];
-        if (++q == inner) {
-            q = 0;
-            ++oo;
-        }
-        if (run != 0 && c == run_byte && k + 1 != len) {
-            ++run;
-            if (run <= 3) {
-                o[p++] = (uint8_t)c;
-            } else if (run == 258) {
-                o[p++] = 255;
-                run = 0;
+        // 2. Eh[r][k] bit j: x = tx0 + 64k + j equals x - 1 (row ty0 + r); Ev[c][k] bit j: y = ty0 +
+        //    64k + j equals y - 1 (column tx0 + c). One ballot per word; lane k keeps word k.
+        {
+            const uint32_t nh = 2 * th, total = nh + 2 * tw;
+            for (uint32_t q0 = 64 * wv; q0 < total; q0 += 256) {
+                uint64_t keep = 0;
+                const uint32_t cnt = total - q0 < 64 ? total - q0 : 64;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const uint32_t q = q0 + k;
+                    bool e;
+                    if (q < nh) {
+                        const uint32_t rr = q >> 1, col = 64 * (q & 1) + lane;
+                        e = col < tw && tx0 + col > 0 &&
+                            D[(rr + 1) * kDS + col + 1] == D[(rr + 1) * kDS + col];
+                    } else {
+                        const uint32_t cc = (q - nh) >> 1, row = 64 * ((q - nh) & 1) + lane;
+                        e = row < th && ty0 + row > 0 && D[(row + 1) * kDS + cc + 1] == D[row * kDS + cc + 1];
+                    }
+                    const uint64_t b = ballot(e);
+                    keep = lane == k ? b : keep;
+                }
+                if (lane < cnt) {
+                    const uint32_t q = q0 + lane;
+                    E[q < nh ? q : 2 * kTile + (q - nh)] = keep;
+                }
             }
-        } else {
-            if (run >= 3) o[p++] = (uint8_t)(run - 3);
-            o[p++] = (uint8_t)c;
-            run_byte = c;
-            run = 1;
+        }
+        __syncthreads();
+        const uint64_t *Eh = E, *Ev = E + 2 * kTile;
+        // 3. blocks of B <= 128, both scan orders
+        const uint32_t nct = M.nc < kTileCand ? M.nc : kTileCand;
+        for (uint32_t c = 0; c < nct; ++c) {
+            const uint32_t B = 8u << c, lg = 3 + c;
+            const uint32_t nbx = (tw + B - 1) >> lg, nby = (th + B - 1) >> lg;
+            const uint32_t per_o = (nbx * nby) << lg, items = 2 * per_o;
+            for (uint32_t base = 0; base < items; base += 256) {
+                const uint32_t it = base + tid;
+                const uint32_t o = it >= per_o, q = it - (o ? per_o : 0u);
+                const uint32_t blk = q >> lg, r = q & (B - 1);
+                const uint32_t bx = blk % nbx, by = blk / nbx;
+                const uint32_t x0 = bx << lg, y0 = by << lg;
+                const uint32_t sx = tw - x0 < B ? tw - x0 : B, sy = th - y0 < B ? th - y0 : B;
+                Seg s = seg_id();
+                if (it < items) {
+                    if (o == 0 && r < sy) {  // block row r (transform.cpp:66-94, horizontal)
+                        const uint32_t y = y0 + r;
+                        const uint32_t first =
+                            r ? (uint32_t)(D[(y + 1) * kDS + x0 + 1] == D[y * kDS + x0 + sx]) : 0u;
+                        s = seg_piece(Eh + 2 * y, x0, sx, first);
+                    } else if (o == 1 && r < sx) {  // block column r (vertical)
+                        const uint32_t x = x0 + r;
+                        const uint32_t first =
+                            r ? (uint32_t)(D[(y0 + 1) * kDS + x + 1] == D[(y0 + sy) * kDS + x]) : 0u;
+                        s = seg_piece(Ev + 2 * x, y0, sy, first);
+                    }
+                }
+                s = seg_group(s, B < 64 ? B : 64u, lane);
+                if (B <= 64) {
+                    if ((lane & (B - 1)) == 0 && it < items) hv[o][blk] = seg_cost(s);
+                } else if (lane == 0) {
+                    part[wv] = s;
+                }
+            }
+            __syncthreads();
+            if (B == 128 && tid < 2) hv[tid][0] = seg_cost(seg_join(part[2 * tid], part[2 * tid + 1]));
+            __syncthreads();
+            // transform.cpp:113-123: the shorter scan, ties horizontal; word = cost | h << 31
+            const uint32_t nblk = nbx * nby;
+            const uint64_t per_row = cdiv(W, B);
+            uint32_t sum = 0;
+            for (uint32_t b = tid; b < nblk; b += 256) {
+                const uint32_t hc = hv[0][b], vc = hv[1][b];
+                const uint64_t gi = (ty0 / B + b / nbx) * per_row + tx0 / B + b % nbx;
+                at<uint32_t>(ws, M.cost0[c])[gi] = hc <= vc ? (hc | 0x80000000u) : vc;
+                sum += hc <= vc ? hc : vc;
+            }
+            for (uint32_t d = 32; d; d >>= 1) sum += __shfl_down(sum, d, 64);
+            if (lane == 0) red[wv] = sum;
+            __syncthreads();
+            if (tid == 0) atomicAdd(&M.total[c], (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
+        }
+        // 4. tile summaries for the blocks of B >= 256
+        if (M.nc > kTileCand) {
+            const uint64_t nty = cdiv(H, kTile);
+            uint64_t *pc = at<uint64_t>(ws, M.pieces);
+            if (tid < th) {
+                const uint64_t *w = Eh + 2 * tid;
+                const Seg s = tw > 1 ? (tw > 64 ? seg_join(seg_leaf(w[0] >> 1, 63), seg_leaf(w[1], tw - 64))
+                                                : seg_leaf(w[0] >> 1, tw - 1))
+                                     : seg_id();
+                pc[(ty0 + tid) * ntx + tx0 / kTile] =
+                    piece_pack(s, (uint32_t)(w[0] & 1), D[(tid + 1) * kDS + 1], D[(tid + 1) * kDS + tw]);
+            } else if (tid >= 128 && tid - 128 < tw) {
+                const uint32_t x = tid - 128;
+                const uint64_t *w = Ev + 2 * x;
+                const Seg s = th > 1 ? (th > 64 ? seg_join(seg_leaf(w[0] >> 1, 63), seg_leaf(w[1], th - 64))
+                                                : seg_leaf(w[0] >> 1, th - 1))
+                                     : seg_id();
+                pc[H * ntx + (tx0 + x) * nty + ty0 / kTile] =
+                    piece_pack(s, (uint32_t)(w[0] & 1), D[kDS + x + 1], D[th * kDS + x + 1]);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ordered join of one Seg per thread over a 256-thread workgroup (thread 0 gets the fold)
+__device__ __forceinline__ Seg seg_block(Seg s, Seg *part, uint32_t tid)
+{
+    s = seg_group(s, 64, tid & 63);
+    if ((tid & 63) == 0) part[tid >> 6] = s;
+    __syncthreads();
+    Seg r = seg_id();
+    if (tid == 0) r = seg_join(seg_join(part[0], part[1]), seg_join(part[2], part[3]));
+    __syncthreads();
+    return r;
+}
+
+// blocks of B >= 256: rows (h) / columns (v) joined from the tile summaries
+__global__ __launch_bounds__(256) void big_cost_kernel(EncArgs a, Ws ws)
+{
+    __shared__ Seg part[4];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t items = ws.ctr[1];
+    for (uint64_t t = blockIdx.x; t < items; t += gridDim.x) {
+        const uint32_t i = find_item(ws.idx[1], a.n, t);
+        AMeta &M = ws.meta[i];
+        if (M.status) continue;
+        uint64_t k = t - ws.idx[1][i];
+        uint32_t c = kTileCand;
+        while (c < kCand - 1 && k >= M.nbc[c]) k -= M.nbc[c++];
+        const uint64_t W = M.w, H = M.h, B = 8ull << c;
+        const uint64_t ntx = cdiv(W, kTile), nty = cdiv(H, kTile), per_row = cdiv(W, B);
+        const uint64_t x0 = (k % per_row) * B, y0 = (k / per_row) * B;
+        const uint64_t sx = W - x0 < B ? W - x0 : B, sy = H - y0 < B ? H - y0 : B;
+        const uint64_t *pc = at<uint64_t>(ws, M.pieces);
+        uint32_t cost[2];
+        for (uint32_t o = 0; o < 2; ++o) {
+            // o = 0: rows y0.. of width sx over tiles x0/128..; o = 1: columns
+            const uint64_t lines = o ? sx : sy, first_line = o ? x0 : y0;
+            const uint64_t t0 = (o ? y0 : x0) / kTile, t1 = ((o ? y0 + sy : x0 + sx) - 1) / kTile;
+            const uint64_t span = o ? H : W;
+            const uint64_t stride = o ? nty : ntx;
+            const uint64_t *P = pc + (o ? H * ntx : 0);
+            const uint64_t per = (lines + 255) / 256;
+            const uint64_t lb = tid * per, le = lb + per < lines ? lb + per : lines;
+            Seg acc = seg_id();
+            for (uint64_t r = lb; r < le; ++r) {
+                const uint64_t line = first_line + r;
+                const uint32_t prev_last = r ? (uint32_t)(P[(line - 1) * stride + t1] >> 40) & 0xFF : 0u;
+                for (uint64_t tt = t0; tt <= t1; ++tt) {
+                    const uint64_t e = P[line * stride + tt];
+                    const uint64_t len = span - tt * kTile < kTile ? span - tt * kTile : kTile;
+                    const uint32_t b0 = tt == t0 ? (r ? (uint32_t)(((e >> 32) & 0xFF) == prev_last) : 0u)
+                                                 : (uint32_t)(e >> 48) & 1u;
+                    acc = seg_join(acc, seg_join(seg_leaf(b0, 1), piece_seg(e, (uint32_t)len - 1)));
+                }
+            }
+            cost[o] = seg_cost(seg_block(acc, part, tid));
+        }
+        if (tid == 0) {
+            const uint32_t hc = cost[0], vc = cost[1];
+            at<uint32_t>(ws, M.cost0[c])[k] = hc <= vc ? (hc | 0x80000000u) : vc;
+            atomicAdd(&M.total[c], (unsigned long long)(hc <= vc ? hc : vc));
         }
     }
 }
 
-// ------------------------------------------------------------------------------ decode ---
+// transform.cpp:309-325 (first minimum of header + data), headers.cpp:18-63 (header), then the
+// winner's block lengths -> their offsets, in place
+__global__ __launch_bounds__(256) void choose_kernel(EncArgs a, Ws ws)
+{
+    __shared__ uint64_t part[256];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+        AMeta &M = ws.meta[i];
+        if (M.status) {
+            if (tid == 0) ws.sym_lens[i] = 0;
+            continue;
+        }
+        uint32_t best = 0;
+        uint64_t best_len = 0;
+        for (uint32_t c = 0; c < M.nc; ++c) {
+            const uint64_t l = 24 + cdiv(M.nbc[c], 8) + M.total[c];
+            if (c == 0 || l < best_len) {
+                best = c;
+                best_len = l;
+            }
+        }
+        const uint64_t nb = M.nbc[best], B = 8ull << best, hdr = 24 + cdiv(nb, 8);
+        uint8_t *sym = at<uint8_t>(ws, M.sym);
+        uint32_t *wd = at<uint32_t>(ws, M.cost0[best]);
+        if (tid < 24) {
+            const uint64_t v = tid < 8 ? M.w : (tid < 16 ? M.h : B);
+            sym[tid] = (uint8_t)(v >> (56 - 8 * (tid % 8)));
+        }
+        for (uint64_t k = tid; k < hdr - 24; k += 256) {  // direction bits, MSB first, 1 = h
+            uint32_t byte = 0;
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint64_t b = 8 * k + j;
+                byte = byte << 1 | (b < nb ? wd[b] >> 31 : 0u);
+            }
+            sym[24 + k] = (uint8_t)byte;
+        }
+        __syncthreads();
+        // exclusive scan of the chosen lengths, written over the words (u32: < 2^32 data bytes)
+        const uint64_t per = (nb + 255) / 256, lb = tid * per, le = lb + per < nb ? lb + per : nb;
+        uint64_t s = 0;
+        for (uint64_t k = lb; k < le; ++k) s += wd[k] & 0x7FFFFFFFu;
+        part[tid] = s;
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t acc = 0;
+            for (uint32_t k = 0; k < 256; ++k) {
+                const uint64_t v = part[k];
+                part[k] = acc;
+                acc += v;
+            }
+        }
+        __syncthreads();
+        s = part[tid];
+        for (uint64_t k = lb; k < le; ++k) {
+            const uint32_t v = wd[k] & 0x7FFFFFFFu;
+            wd[k] = (uint32_t)s;
+            s += v;
+        }
+        if (tid == 0) {
+            M.nb = nb;
+            M.B = B;
+            M.best = best;
+            M.hdr = hdr;
+            M.count = best_len;
+            if (M.total[best] >= 0xFFFFFFFFull) M.status = HC_ERR_UNSUPPORTED;
+            ws.sym_lens[i] = M.status ? 0 : best_len;
+        }
+        __syncthreads();
+    }
+}
 
-// Where each block's RLE data starts (transform.cpp:330-361 running revertRLEBlock,
-// transform.cpp:162-187, block by block), reporting 13 / 14 / 15 exactly where the reference
-// exits. One wavefront, 256 symbols per step (4 per lane). The revert machine's state r (0..3:
-// how many equal literals precede; 3 = the next symbol is a count) moves by one of two functions
-// per symbol — a literal repeating the previous symbol (r -> r + 1) or not (r -> 1), a count -> 0;
-// from 0 both give 1, so the symbol before a block start never matters. A wave scan of their
-// compositions gives each symbol's state, hence its output length (count: the symbol, literal:
-// 1); a scan of lengths finds the first symbol where the block's byte count is reached. A block
-// that ends inside the step re-scans the rest of the same registers from state 0.
-constexpr uint32_t kFsmEq = 1u | 2u << 2 | 3u << 4;        // r: 0->1 1->2 2->3 3->0
-constexpr uint32_t kFsmNe = 1u | 1u << 2 | 1u << 4;        // r: 0->1 1->1 2->1 3->0
+// q / d for q < 2^24 (block-relative positions of the encoder: blocks <= 1024 x 1024)
+__device__ __forceinline__ uint32_t div_small(uint32_t q, uint32_t d, float inv)
+{
+    uint32_t r = (uint32_t)((float)q * inv);
+    r -= r * d > q;
+    r += (r + 1) * d <= q;
+    return r;
+}
+
+// transform.cpp:241-279 for one block's scan per wave, 64 elements per step (model:
+// tests/adapt_cost_model.py emit_lanes)
+__global__ __launch_bounds__(256) void emit_kernel(EncArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t items = ws.ctr[2];
+    const uint64_t lt = lanes_below(lane);
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
+        const uint32_t i = find_item(ws.idx[2], a.n, t);
+        const AMeta &M = ws.meta[i];
+        const uint64_t k = t - ws.idx[2][i];
+        if (M.status || k >= M.nb) continue;
+        const uint64_t W = M.w, H = M.h, B = M.B;
+        const uint64_t per_row = cdiv(W, B);
+        const uint64_t x0 = (k % per_row) * B, y0 = (k / per_row) * B;
+        const uint32_t sx = (uint32_t)(W - x0 < B ? W - x0 : B), sy = (uint32_t)(H - y0 < B ? H - y0 : B);
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        const bool horiz = (sym[24 + k / 8] >> (7 - k % 8)) & 1;
+        uint8_t *out = at<uint8_t>(ws, M.sym) + M.hdr + at<uint32_t>(ws, M.cost0[M.best])[k];
+        const uint8_t *mat = a.in + a.in_offs[i];
+        const bool diff = a.diff != 0;
+        const uint32_t inner = horiz ? sx : sy;
+        const float inv = 1.0f / (float)inner;
+        const uint32_t L = sx * sy;
+        auto value = [&](uint32_t p) -> uint32_t {
+            const uint32_t a1 = div_small(p, inner, inv), b1 = p - a1 * inner;
+            const uint64_t x = x0 + (horiz ? b1 : a1), y = y0 + (horiz ? a1 : b1);
+            const uint64_t lin = y * W + x;
+            uint32_t v = mat[lin];
+            if (diff) v = (v - (lin ? mat[lin - 1] : 0u)) & 0xFFu;
+            return v;
+        };
+        uint32_t pv = 0, po = 0;  // value and run offset of the previous step's last element
+        uint64_t q = 0;           // bytes written
+        for (uint32_t base = 0; base < L; base += 64) {
+            const uint32_t p = base + lane;
+            const bool valid = p < L;
+            const uint32_t v = valid ? value(p) : 0u;
+            uint32_t prev = __shfl_up(v, 1, 64);
+            if (lane == 0) prev = pv;
+            uint32_t nx = __shfl_down(v, 1, 64);
+            if (lane == 63 && p + 1 < L) nx = value(p + 1);
+            const bool start = p == 0 || v != prev;
+            const uint64_t sm = ballot(valid && start);
+            const uint64_t le = sm & (lt | (1ull << lane));
+            const uint32_t o = le ? lane - (63u - (uint32_t)__builtin_clzll(le)) : po + 1 + lane;
+            const uint32_t j = o % 258u;
+            const bool last = p + 1 == L;
+            const bool end = p + 2 == L || (p + 2 < L && nx != v);
+            uint32_t cnt = last ? 1u : (uint32_t)(j <= 2) + (uint32_t)(j == 257) + (uint32_t)(end && j >= 2 && j <= 256);
+            if (!valid) cnt = 0;
+            const uint64_t b1 = ballot(cnt >= 1), b2 = ballot(cnt == 2);
+            const uint64_t pos = q + __popcll(b1 & lt) + __popcll(b2 & lt);
+            const uint32_t first = (last || j <= 2) ? v : (j == 257 ? 255u : j - 2);
+            if (cnt >= 1) out[pos] = (uint8_t)first;
+            if (cnt == 2) out[pos + 1] = 0;
+            q += __popcll(b1) + __popcll(b2);
+            po = __shfl(o, 63, 64);
+            pv = __shfl(v, 63, 64);
+        }
+    }
+}
+
+// adaptive failures (4 / 6 / 12 / capacity) replace whatever the FGK stage reported
+__global__ void status_fix_kernel(Ws ws, uint32_t n, int32_t *status, uint64_t *out_lens)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && ws.meta[i].status) {
+        status[i] = ws.meta[i].status;
+        out_lens[i] = 0;
+    }
+}
+
+// --------------------------------------------------------------------------- decode ------
+
+struct DecArgs {
+    const uint8_t *in;
+    const uint64_t *in_offs, *in_lens;
+    uint32_t n;
+    uint8_t *out;
+    const uint64_t *out_offs, *out_caps;
+    uint64_t *out_lens;
+    int32_t *status;
+};
+
+__device__ __forceinline__ uint64_t group_entries_bound(uint64_t cap) { return cap / 256 + 2; }
+
+// symbols the FGK stage may write: the count, unless the payload cannot hold it (the first symbol
+// takes >= 8 bits, every later one >= 1), which the FGK decoder reports as 9 without writing
+__device__ __forceinline__ uint64_t sym_cap(uint64_t count, uint64_t len)
+{
+    const uint64_t avail = (len - 9) * 8;
+    return count > (avail >= 8 ? avail - 7 : 0) ? 0 : count;
+}
+
+// headers of the outer stream (main.cpp:90-104): symbol capacity per stream
+__global__ __launch_bounds__(1024) void dec_plan_kernel(DecArgs a, Ws ws)
+{
+    auto need = [&](uint32_t i, uint64_t *v) {
+        const uint64_t len = a.in_lens[i];
+        const uint8_t *p = a.in + a.in_offs[i];
+        uint64_t count = 0;
+        if (len >= 9)
+            for (int b = 7; b >= 0; --b) count = count << 8 | p[b];
+        const bool ok = len >= 9 && (p[8] & HC_FLAG_ADAPT);
+        const uint64_t oc = a.out_caps[i];
+        v[0] = ok ? align_up(sym_cap(count, len) + 64, 16) + align_up(8 * group_entries_bound(oc) + oc / kChunk + 16, 16)
+                  : 0;
+    };
+    auto put = [&](uint32_t i, const uint64_t *base) {
+        uint64_t v[1];
+        need(i, v);
+        AMeta &m = ws.meta[i];
+        const uint64_t len = a.in_lens[i];
+        const uint8_t *p = a.in + a.in_offs[i];
+        m.status = len < 9 ? HC_ERR_HEADER : ((p[8] & HC_FLAG_ADAPT) ? 0 : HC_ERR_UNSUPPORTED);
+        m.diff = len >= 9 ? (p[8] & HC_FLAG_DIFF) != 0 : 0;
+        m.slab = ws.slab0 + base[0];
+        if (m.status == 0 && m.slab + v[0] > ws.slab_end) m.status = HC_ERR_CAPACITY;
+        m.sym = m.slab;
+        uint64_t count = 0;
+        if (len >= 9)
+            for (int b = 7; b >= 0; --b) count = count << 8 | p[b];
+        const uint64_t cap = m.status ? 0 : sym_cap(count, len);
+        m.starts = m.slab + align_up(cap + 64, 16);
+        m.csum = m.starts + 8 * group_entries_bound(a.out_caps[i]);
+        ws.sym_offs[i] = m.sym;
+        ws.sym_caps[i] = cap;
+        ws.sym_lens[i] = 0;
+        ws.lens2[i] = m.status ? 0 : len;
+    };
+    __shared__ uint64_t tot[1];
+    wg_scan<1>(a.n, need, put, tot);
+}
+
+// headers.cpp:65-105 on the decoded symbols, then the unblock groups and undiff chunks
+__global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
+{
+    auto parse = [&](uint32_t i) {
+        AMeta &m = ws.meta[i];
+        m.nb = m.groups = m.chunks = 0;
+        if (m.status == 0 && a.status[i] != 0) m.status = a.status[i];  // the FGK stage's (8 / 9 / ...)
+        if (m.status) return;
+        const uint64_t count = ws.sym_lens[i];
+        const uint8_t *s = at<uint8_t>(ws, m.sym);
+        m.count = count;
+        if (count < 24) {  // headers.cpp:67-71
+            m.status = HC_ERR_ADAPT_HEADER;
+            return;
+        }
+        uint64_t f[3] = {0, 0, 0};
+        for (int k = 0; k < 3; ++k)
+            for (int b = 0; b < 8; ++b) f[k] = f[k] << 8 | s[8 * k + b];
+        const uint64_t w = f[0], h = f[1], b = f[2];
+        if (b == 0) {  // transform.cpp:415 divides by it (the reference dies by SIGFPE)
+            m.status = HC_ERR_BLOCK_SIZE;
+            return;
+        }
+        const uint64_t nb = nblocks(w, h, b);
+        if (count - 24 < cdiv(nb, 8)) {  // headers.cpp:94-98
+            m.status = HC_ERR_ADAPT_DIRS;
+            return;
+        }
+        if (w != 0 && h > (1ull << 36) / w) {  // the reference: bad_alloc
+            m.status = HC_ERR_TOO_LARGE;
+            return;
+        }
+        m.w = w;
+        m.h = h;
+        m.B = b;
+        m.nb = nb;
+        m.hdr = 24 + cdiv(nb, 8);
+        if (w * h > a.out_caps[i]) {
+            m.status = HC_ERR_CAPACITY;
+            a.out_lens[i] = w * h;
+            return;
+        }
+        const uint64_t bx = b < w ? b : w, by = b < h ? b : h;
+        const uint64_t area = bx * by;
+        m.K = area >= kGroupBytes ? 1 : cdiv(kGroupBytes, area ? area : 1);
+        m.groups = cdiv(nb, m.K);
+        m.chunks = m.diff ? cdiv(w * h, kChunk) : 0;
+    };
+    for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) parse(i);
+    __syncthreads();
+    auto need = [&](uint32_t i, uint64_t *v) {
+        v[0] = ws.meta[i].status ? 0 : ws.meta[i].groups;
+        v[1] = ws.meta[i].status ? 0 : ws.meta[i].chunks;
+        v[2] = ws.meta[i].status ? 0 : 1;
+    };
+    auto put = [&](uint32_t i, const uint64_t *base) {
+        ws.idx[0][i] = base[0];
+        ws.idx[1][i] = base[1];
+    };
+    __shared__ uint64_t tot[3];
+    wg_scan<3>(a.n, need, put, tot);
+    if (threadIdx.x == 0) {
+        ws.idx[0][a.n] = tot[0];
+        ws.idx[1][a.n] = tot[1];
+        ws.ctr[0] = tot[0];
+        ws.ctr[1] = tot[1];
+    }
+}
+
+// The revert machine (transform.cpp:137-159) as state r in 0..3 (equal literals seen; 3 = the
+// next symbol is a count): a literal equal to the previous symbol moves r -> r + 1, another one
+// r -> 1, a count 3 -> 0; from 0 both give 1, so the symbol before a block start never matters.
+// Transition functions as 4 x 2-bit tables, composed by wave scans.
+constexpr uint32_t kFsmEq = 1u | 2u << 2 | 3u << 4;  // 0->1 1->2 2->3 3->0
+constexpr uint32_t kFsmNe = 1u | 1u << 2 | 1u << 4;  // 0->1 1->1 2->1 3->0
 constexpr uint32_t kFsmId = 0u | 1u << 2 | 2u << 4 | 3u << 6;
 
 __device__ __forceinline__ uint32_t fsm_then(uint32_t g, uint32_t f)  // x -> g(f(x))
@@ -275,339 +864,360 @@ __device__ __forceinline__ uint32_t fsm_then(uint32_t g, uint32_t f)  // x -> g(
     return h;
 }
 
-__global__ __launch_bounds__(64) void bounds_kernel(const uint8_t *sym, uint64_t nsym, uint64_t w,
-                                                    uint64_t h, uint64_t b, uint64_t nb, uint64_t pos0,
-                                                    uint64_t *start, int *status)
+__device__ __forceinline__ uint32_t block_size(const AMeta &m, uint64_t k, uint64_t *x0, uint64_t *y0,
+                                               uint64_t *sx, uint64_t *sy)
 {
-    const uint32_t lane = threadIdx.x;
-    uint64_t pos = pos0;  // first symbol of the loaded step
-    uint64_t blk = 0, got = 0;
-    uint32_t r = 0, last = 0;  // machine state and previous symbol at the step's start
-    if (lane == 0) start[0] = pos;
-    uint64_t want = 0;
-    if (nb) {
-        const Geo g = block_geo(w, h, b, 0);
-        want = g.sx * g.sy;
-    }
-    while (blk < nb) {
-        const uint64_t avail = nsym - pos;
-        const uint32_t m = avail < 256 ? (uint32_t)avail : 256u;
-        if (m == 0) {  // transform.cpp:170-174: the block wants more, the stream is empty
-            if (lane == 0) *status = HC_ERR_BLOCK_EOF;
-            return;
+    const uint64_t per_row = cdiv(m.w, m.B);
+    *x0 = (k % per_row) * m.B;
+    *y0 = (k / per_row) * m.B;
+    *sx = m.w - *x0 < m.B ? m.w - *x0 : m.B;
+    *sy = m.h - *y0 < m.B ? m.h - *y0 : m.B;
+    return 0;
+}
+
+// Where the blocks start (transform.cpp:330-361 running revertRLEBlock, transform.cpp:162-187,
+// block by block), reporting 13 / 14 / 15 exactly where the reference exits. One wave per
+// stream, 256 symbols per step (4 per lane); a scan of the transition functions gives each
+// symbol's state, hence its output length (count: the symbol, literal: 1); a scan of lengths
+// finds the first symbol where the block's byte count is reached. A block that ends inside the
+// step re-scans the rest of the same registers from state 0. The start of every K-th block is
+// recorded for the unblock waves.
+__global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    for (uint32_t i = blockIdx.x * 4 + wv; i < a.n; i += gridDim.x * 4) {
+        AMeta &M = ws.meta[i];
+        if (M.status) continue;
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        uint64_t *starts = at<uint64_t>(ws, M.starts);
+        const uint64_t nsym = M.count, nb = M.nb, K = M.K;
+        uint64_t pos = M.hdr;
+        uint64_t blk = 0, got = 0;
+        uint32_t r = 0, last = 0;
+        int status = 0;
+        if (lane == 0 && nb) starts[0] = pos;
+        uint64_t want = 0;
+        if (nb) {
+            uint64_t x0, y0, sx, sy;
+            block_size(M, 0, &x0, &y0, &sx, &sy);
+            want = sx * sy;
         }
-        uint32_t x[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) x[k] = 4 * lane + k < m ? sym[pos + 4 * lane + k] : 0u;
-        const uint32_t up = __shfl_up(x[3], 1, 64);
-        uint32_t lo = 0;  // symbols below lo belong to blocks already closed
-        for (;;) {
-            uint32_t f[4], F = kFsmId;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t i = 4 * lane + k;
-                const uint32_t p = k ? x[k - 1] : (lane ? up : last);
-                f[k] = (i >= lo && i < m) ? (x[k] == p ? kFsmEq : kFsmNe) : kFsmId;
-                F = fsm_then(f[k], F);
+        while (blk < nb) {
+            const uint64_t avail = nsym - pos;
+            const uint32_t m = avail < 256 ? (uint32_t)avail : 256u;
+            if (m == 0) {  // transform.cpp:170-174: the block wants more, the stream is empty
+                status = HC_ERR_BLOCK_EOF;
+                break;
             }
-            uint32_t inc = F;
-            for (uint32_t off = 1; off < 64; off <<= 1) {
-                const uint32_t g = __shfl_up(inc, off, 64);
-                inc = lane >= off ? fsm_then(inc, g) : inc;
-            }
-            const uint32_t ex = __shfl_up(inc, 1, 64);
-            uint32_t s = ((lane ? ex : kFsmId) >> (2 * r)) & 3u;
-            uint32_t len[4], tot = 0;
+            uint32_t x[4];
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t i = 4 * lane + k;
-                len[k] = (i >= lo && i < m) ? (s == 3 ? x[k] : 1u) : 0u;
-                tot += len[k];
-                s = (f[k] >> (2 * s)) & 3u;
+            for (uint32_t k = 0; k < 4; ++k) x[k] = 4 * lane + k < m ? sym[pos + 4 * lane + k] : 0u;
+            const uint32_t up = __shfl_up(x[3], 1, 64);
+            uint32_t lo = 0;  // symbols below lo belong to blocks already closed
+            bool stop = false;
+            for (;;) {
+                uint32_t f[4], F = kFsmId;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t ii = 4 * lane + k;
+                    const uint32_t p = k ? x[k - 1] : (lane ? up : last);
+                    f[k] = (ii >= lo && ii < m) ? (x[k] == p ? kFsmEq : kFsmNe) : kFsmId;
+                    F = fsm_then(f[k], F);
+                }
+                uint32_t inc = F;
+                for (uint32_t off = 1; off < 64; off <<= 1) {
+                    const uint32_t g = __shfl_up(inc, off, 64);
+                    inc = lane >= off ? fsm_then(inc, g) : inc;
+                }
+                const uint32_t ex = __shfl_up(inc, 1, 64);
+                uint32_t s = ((lane ? ex : kFsmId) >> (2 * r)) & 3u;
+                uint32_t len[4], tot = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t ii = 4 * lane + k;
+                    len[k] = (ii >= lo && ii < m) ? (s == 3 ? x[k] : 1u) : 0u;
+                    tot += len[k];
+                    s = (f[k] >> (2 * s)) & 3u;
+                }
+                uint32_t acc = tot;
+                for (uint32_t off = 1; off < 64; off <<= 1) {
+                    const uint32_t g = __shfl_up(acc, off, 64);
+                    acc += lane >= off ? g : 0u;
+                }
+                const uint64_t need = want - got;  // >= 1
+                const uint64_t hit = ballot((uint64_t)acc >= need);
+                if (!hit) {  // the block goes on past this step
+                    got += __shfl(acc, 63, 64);
+                    r = (__shfl(inc, 63, 64) >> (2 * r)) & 3u;
+                    last = __shfl(x[(m - 1) & 3u], (m - 1) >> 2, 64);
+                    pos += m;
+                    break;
+                }
+                const uint32_t L = (uint32_t)__builtin_ctzll(hit);
+                uint32_t c = acc - tot, j = 0xFFFFFFFFu, cj = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    c += len[k];
+                    if (j == 0xFFFFFFFFu && (uint64_t)c >= need) {
+                        j = 4 * lane + k;
+                        cj = c;
+                    }
+                }
+                j = __shfl(j, L, 64);
+                cj = __shfl(cj, L, 64);
+                if ((uint64_t)cj != need) {  // transform.cpp:178-182: a count overshoots the block
+                    status = HC_ERR_BLOCK_DATA;
+                    stop = true;
+                    break;
+                }
+                lo = j + 1;
+                ++blk;
+                if (blk < nb && blk % K == 0 && lane == 0) starts[blk / K] = pos + lo;
+                if (blk == nb) {
+                    pos += lo;
+                    break;
+                }
+                uint64_t x0, y0, sx, sy;
+                block_size(M, blk, &x0, &y0, &sx, &sy);
+                want = sx * sy;
+                got = 0;
+                r = 0;
+                if (lo == m) {
+                    pos += m;
+                    break;
+                }
             }
-            uint32_t acc = tot;  // inclusive scan of lengths (<= 256 * 255)
+            if (stop) break;
+        }
+        if (status == 0 && pos != nsym) status = HC_ERR_LEFTOVER;  // transform.cpp:354-358
+        if (lane == 0) M.status = status;
+    }
+}
+
+// transform.cpp:162-216 for the blocks of one group per wave: revert each block's RLE from its
+// start with a fresh machine, 64 symbols per step, and scatter the bytes in scan order.
+__global__ __launch_bounds__(256) void unblock_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t items = ws.ctr[0];
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
+        const uint32_t i = find_item(ws.idx[0], a.n, t);
+        const AMeta &M = ws.meta[i];
+        if (M.status) continue;
+        const uint64_t g = t - ws.idx[0][i];
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        const uint8_t *dirs = sym + 24;
+        uint64_t pos = at<uint64_t>(ws, M.starts)[g];
+        uint8_t *mat = a.out + a.out_offs[i];
+        const uint64_t W = M.w;
+        const uint64_t kb = g * M.K, ke = kb + M.K < M.nb ? kb + M.K : M.nb;
+        for (uint64_t k = kb; k < ke; ++k) {
+            uint64_t x0, y0, sx, sy;
+            block_size(M, k, &x0, &y0, &sx, &sy);
+            const bool horiz = (dirs[k / 8] >> (7 - k % 8)) & 1;
+            const uint64_t inner = horiz ? sx : sy, want = sx * sy;
+            const bool small = want < (1u << 24);
+            const float inv = 1.0f / (float)inner;
+            auto place = [&](uint64_t q, uint32_t v) {
+                uint64_t a1, b1;
+                if (small) {
+                    a1 = div_small((uint32_t)q, (uint32_t)inner, inv);
+                } else {
+                    a1 = q / inner;
+                }
+                b1 = q - a1 * inner;
+                const uint64_t x = x0 + (horiz ? b1 : a1), y = y0 + (horiz ? a1 : b1);
+                mat[y * W + x] = (uint8_t)v;
+            };
+            uint64_t got = 0;
+            uint32_t r = 0, last = 0;
+            while (got < want && pos < M.count) {  // (the bounds pass proved the block whole)
+                const uint32_t xs = sym[pos + lane];  // in range: the bounds pass proved the block whole
+                const uint32_t up = __shfl_up(xs, 1, 64);
+                const uint32_t pr = lane ? up : last;
+                const uint32_t f = xs == pr ? kFsmEq : kFsmNe;
+                uint32_t inc = f;
+                for (uint32_t off = 1; off < 64; off <<= 1) {
+                    const uint32_t gg = __shfl_up(inc, off, 64);
+                    inc = lane >= off ? fsm_then(inc, gg) : inc;
+                }
+                const uint32_t ex = __shfl_up(inc, 1, 64);
+                const uint32_t s = ((lane ? ex : kFsmId) >> (2 * r)) & 3u;
+                const uint32_t len = s == 3 ? xs : 1u;
+                const uint32_t val = s == 3 ? pr : xs;  // a count repeats the literal before it
+                uint32_t acc = len;
+                for (uint32_t off = 1; off < 64; off <<= 1) {
+                    const uint32_t gg = __shfl_up(acc, off, 64);
+                    acc += lane >= off ? gg : 0u;
+                }
+                const uint64_t need = want - got;
+                const uint64_t hit = ballot((uint64_t)acc >= need);
+                const uint32_t L = hit ? (uint32_t)__builtin_ctzll(hit) : 63u;  // last lane of this block
+                const bool mine = lane <= L;
+                const uint64_t q0 = got + acc - len;
+                uint32_t mx = mine ? len : 0u;
+                for (uint32_t d = 32; d; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+                for (uint32_t e = 0; e < mx; ++e)
+                    if (mine && e < len) place(q0 + e, val);
+                got += __shfl(acc, L, 64);
+                r = (__shfl(inc, L, 64) >> (2 * r)) & 3u;
+                last = __shfl(xs, L, 64);
+                pos += L + 1;
+            }
+        }
+    }
+}
+
+// transform.cpp:231-239 (prefix sum mod 256 over the linear matrix) in 16 KB chunks:
+// per-chunk byte sums, a per-stream scan of those, then the chunks' prefix sums
+__global__ __launch_bounds__(256) void chunk_sum_kernel(DecArgs a, Ws ws)
+{
+    __shared__ uint32_t red[4];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t items = ws.ctr[1];
+    for (uint64_t t = blockIdx.x; t < items; t += gridDim.x) {
+        const uint32_t i = find_item(ws.idx[1], a.n, t);
+        const AMeta &M = ws.meta[i];
+        const uint64_t c = t - ws.idx[1][i], n = M.w * M.h;
+        const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
+        const uint8_t *mat = a.out + a.out_offs[i];
+        uint32_t s = 0;
+        for (uint64_t k = b + tid; k < e; k += 256) s += mat[k];
+        for (uint32_t d = 32; d; d >>= 1) s += __shfl_down(s, d, 64);
+        if ((tid & 63) == 0) red[tid >> 6] = s;
+        __syncthreads();
+        if (tid == 0) at<uint8_t>(ws, M.csum)[c] = (uint8_t)(red[0] + red[1] + red[2] + red[3]);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64) void chunk_scan_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id();
+    for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+        const AMeta &M = ws.meta[i];
+        if (M.status || !M.chunks) continue;
+        uint8_t *cs = at<uint8_t>(ws, M.csum);
+        uint32_t carry = 0;
+        for (uint64_t b = 0; b < M.chunks; b += 64) {
+            const bool ok = b + lane < M.chunks;
+            const uint32_t v = ok ? cs[b + lane] : 0u;
+            uint32_t acc = v;
             for (uint32_t off = 1; off < 64; off <<= 1) {
                 const uint32_t g = __shfl_up(acc, off, 64);
                 acc += lane >= off ? g : 0u;
             }
-            const uint64_t need = want - got;  // >= 1
-            const uint64_t hit = __ballot((uint64_t)acc >= need);
-            if (!hit) {  // the block goes on past this step
-                got += __shfl(acc, 63, 64);
-                r = (__shfl(inc, 63, 64) >> (2 * r)) & 3u;
-                const uint32_t lt = __shfl(x[(m - 1) & 3u], (m - 1) >> 2, 64);
-                last = lt;
-                pos += m;
-                break;
-            }
-            // the first symbol whose running length reaches the block's size closes it
-            const uint32_t L = (uint32_t)__builtin_ctzll(hit);
-            uint32_t c = acc - tot, j = 0xFFFFFFFFu, cj = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                c += len[k];
-                if (j == 0xFFFFFFFFu && (uint64_t)c >= need) {
-                    j = 4 * lane + k;
-                    cj = c;
-                }
-            }
-            j = __shfl(j, L, 64);
-            cj = __shfl(cj, L, 64);
-            if ((uint64_t)cj != need) {  // transform.cpp:178-182: a count overshoots the block
-                if (lane == 0) *status = HC_ERR_BLOCK_DATA;
-                return;
-            }
-            lo = j + 1;
-            ++blk;
-            if (lane == 0) start[blk] = pos + lo;
-            if (blk == nb) {
-                pos += lo;
-                break;
-            }
-            const Geo g = block_geo(w, h, b, blk);
-            want = g.sx * g.sy;
-            got = 0;
-            r = 0;
-            if (lo == m) {
-                pos += m;
-                break;
-            }
+            if (ok) cs[b + lane] = (uint8_t)(carry + acc - v);  // exclusive
+            carry += __shfl(acc, 63, 64);
         }
     }
-    // transform.cpp:354-358
-    if (lane == 0) *status = pos != nsym ? HC_ERR_LEFTOVER : 0;
 }
 
-// transform.cpp:162-216 for one block per lane: revert its RLE and scatter in scan order
-__global__ void unblock_kernel(const uint8_t *sym, uint64_t w, uint64_t h, uint64_t b,
-                               uint64_t nb, const uint8_t *dirbits, const uint64_t *start,
-                               uint8_t *m)
+__global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
 {
-    const uint64_t blk = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (blk >= nb) return;
-    const Geo g = block_geo(w, h, b, blk);
-    const bool horiz = (dirbits[blk / 8] >> (7 - blk % 8)) & 1;
-    const uint64_t inner = horiz ? g.sx : g.sy;
-    const uint64_t want = g.sx * g.sy;
-    uint64_t pos = start[blk], got = 0, oo = 0, q = 0;
-    uint32_t run_byte = 0, run = 0;
-    auto put = [&](uint32_t v) {
-        const uint64_t x = horiz ? q : oo, y = horiz ? oo : q;
-        m[(g.y0 + y) * w + g.x0 + x] = (uint8_t)v;
-        if (++q == inner) {
-            q = 0;
-            ++oo;
-        }
-        ++got;
-    };
-    while (got < want) {
-        const uint32_t c = sym[pos++];
-        if (run == 3) {
-            for (uint32_t r = 0; r < c; ++r) put(run_byte);
-            run = 0;
-        } else {
-            put(c);
-            if (c == run_byte) ++run;
-            else {
-                run_byte = c;
-                run = 1;
+    __shared__ uint32_t part[256];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t items = ws.ctr[1];
+    for (uint64_t t = blockIdx.x; t < items; t += gridDim.x) {
+        const uint32_t i = find_item(ws.idx[1], a.n, t);
+        const AMeta &M = ws.meta[i];
+        const uint64_t c = t - ws.idx[1][i], n = M.w * M.h;
+        const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
+        uint8_t *mat = a.out + a.out_offs[i];
+        // 64 bytes per thread, in order
+        const uint64_t tb = b + 64ull * tid, te = tb + 64 < e ? tb + 64 : e;
+        uint32_t s = 0;
+        for (uint64_t k = tb; k < te; ++k) s += mat[k];
+        part[tid] = s;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t acc = at<uint8_t>(ws, M.csum)[c];
+            for (uint32_t k = 0; k < 256; ++k) {
+                const uint32_t v = part[k];
+                part[k] = acc;
+                acc += v;
             }
         }
+        __syncthreads();
+        uint32_t run = part[tid];
+        for (uint64_t k = tb; k < te; ++k) {
+            run += mat[k];
+            mat[k] = (uint8_t)run;
+        }
+        __syncthreads();
     }
 }
 
-// transform.cpp:220-229, out of place
-__global__ void diff_kernel(const uint8_t *in, uint8_t *out, uint64_t n)
+__global__ void dec_final_kernel(DecArgs a, Ws ws)
 {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        out[i] = (uint8_t)(in[i] - (i ? in[i - 1] : 0));
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const AMeta &M = ws.meta[i];
+    a.status[i] = M.status;
+    if (M.status == 0) a.out_lens[i] = M.w * M.h;
+    else if (M.status != HC_ERR_CAPACITY) a.out_lens[i] = 0;
 }
-
-struct ByteAdd {
-    __device__ __forceinline__ uint8_t operator()(uint8_t a, uint8_t b) const
-    {
-        return (uint8_t)(a + b);
-    }
-};
-
-uint64_t ceil_div(uint64_t a, uint64_t b) { return a / b + (a % b != 0); }
-
-#define HC_TRY(x)                          \
-    do {                                   \
-        hipError_t e_ = (x);               \
-        if (e_ != hipSuccess) return e_;   \
-    } while (0)
 
 }  // namespace
 
-hipError_t diff_apply(uint8_t *d, uint64_t n, hipStream_t st)
+uint64_t adapt_encode_work_bound(uint64_t total_in, uint32_t n)
 {
-    if (n == 0) return hipSuccess;
-    uint8_t *tmp = nullptr;
-    HC_TRY(hipMalloc((void **)&tmp, n));
-    HC_TRY(hipMemcpyAsync(tmp, d, n, hipMemcpyDeviceToDevice, st));
-    const uint64_t blocks = ceil_div(n, 256) < 8192 ? ceil_div(n, 256) : 8192;
-    diff_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(tmp, d, n);
-    HC_TRY(hipGetLastError());
-    return hipFree(tmp);
+    // per matrix of L bytes: cost words <= L/3, tile summaries <= 0.19 L, symbols <= 1.41 L + 42
+    return ws_header(n) + 2 * total_in + 128ull * n + 4096;
 }
 
-// transform.cpp:231-239: inclusive prefix sum mod 256
-hipError_t diff_revert(uint8_t *d, uint64_t n, hipStream_t st)
+uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t n)
 {
-    if (n == 0) return hipSuccess;
-    size_t tmp_bytes = 0;
-    HC_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, d, d, ByteAdd(), (int)n, st));
-    void *tmp = nullptr;
-    HC_TRY(hipMalloc(&tmp, tmp_bytes + 16));
-    HC_TRY(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, d, d, ByteAdd(), (int)n, st));
-    return hipFree(tmp);
+    // symbols <= 8 bits each of the payload; group starts <= W*H / 256 + 2; chunk sums
+    return ws_header(n) + 8 * total_in + total_out / 16 + 128ull * n + 4096;
 }
 
-hipError_t adapt_bound(uint64_t n, uint64_t width, uint64_t *bytes)
+hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work, uint64_t work_bytes,
+                              hipStream_t st)
 {
-    (void)width;
-    *bytes = 24 + n / 64 + 64 + n + n / 3 + n / 64 + 64;
-    return hipSuccess;
+    if (b.n == 0) return hipSuccess;
+    const Ws ws = carve(work, work_bytes, b.n);
+    const EncArgs a{b.in, b.in_offs, b.in_lens, widths, b.n, (b.flags & HC_FLAG_DIFF) ? 1u : 0u};
+    enc_plan_kernel<<<1, 1024, 0, st>>>(a, ws);
+    tile_cost_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    big_cost_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    choose_kernel<<<b.n < kGrid ? b.n : kGrid, 256, 0, st>>>(a, ws);
+    emit_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    Batch f = b;
+    f.in = ws.base;
+    f.in_offs = ws.sym_offs;
+    f.in_lens = ws.sym_lens;
+    f.flags = (b.flags & HC_FLAG_DIFF) | HC_FLAG_ADAPT;
+    e = launch_encode(f, SRC_SYMBOLS, st);
+    if (e != hipSuccess) return e;
+    status_fix_kernel<<<(b.n + 255) / 256, 256, 0, st>>>(ws, b.n, b.status, b.out_lens);
+    return hipGetLastError();
 }
 
-// transform.cpp:294-328. Synchronous (the block-size choice is made on the host).
-hipError_t adapt_encode(const uint8_t *m, uint64_t w, uint64_t h, uint8_t *out, uint64_t *d_out_len,
-                        uint64_t *h_block, hipStream_t st)
+hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, hipStream_t st)
 {
-    std::vector<uint64_t> sizes;
-    for (uint64_t b = 8, step = 0; step <= 7 && b <= w && b <= h; ++step, b *= 2) sizes.push_back(b);
-    const size_t nc = sizes.size();
-    const uint64_t nb8 = ceil_div(w, 8) * ceil_div(h, 8);
-    uint64_t *cost = nullptr, *len = nullptr, *off = nullptr;
-    uint8_t *dir = nullptr;
-    unsigned long long *total = nullptr;
-    HC_TRY(hipMalloc((void **)&cost, nb8 * 2 * sizeof(uint64_t)));
-    HC_TRY(hipMalloc((void **)&len, nb8 * sizeof(uint64_t)));
-    HC_TRY(hipMalloc((void **)&off, (nb8 + 1) * sizeof(uint64_t)));
-    HC_TRY(hipMalloc((void **)&dir, nb8));
-    HC_TRY(hipMalloc((void **)&total, nc * sizeof(unsigned long long)));
-    HC_TRY(hipMemsetAsync(total, 0, nc * sizeof(unsigned long long), st));
-    for (size_t c = 0; c < nc; ++c) {
-        const uint64_t b = sizes[c];
-        const uint64_t nb = ceil_div(w, b) * ceil_div(h, b);
-        block_cost_kernel<<<dim3((unsigned)nb, 2), dim3(b * b >= 4 * kCostThreads ? kCostThreads : 64), 0,
-                            st>>>(m, w, h, b, cost);
-        HC_TRY(hipGetLastError());
-        const unsigned g = (unsigned)(ceil_div(nb, 256) < 1024 ? ceil_div(nb, 256) : 1024);
-        choose_kernel<<<dim3(g), dim3(256), 0, st>>>(cost, nb, len, dir, total + c);
-        HC_TRY(hipGetLastError());
-    }
-    std::vector<unsigned long long> tot(nc);
-    HC_TRY(hipMemcpyAsync(tot.data(), total, nc * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    HC_TRY(hipStreamSynchronize(st));
-    // transform.cpp:309-325: first strictly smaller (header + data) wins
-    size_t best = 0;
-    uint64_t best_len = 0;
-    for (size_t c = 0; c < nc; ++c) {
-        const uint64_t nb = ceil_div(w, sizes[c]) * ceil_div(h, sizes[c]);
-        const uint64_t l = 24 + ceil_div(nb, 8) + tot[c];
-        if (c == 0 || l < best_len) {
-            best = c;
-            best_len = l;
-        }
-    }
-    const uint64_t b = sizes[best];
-    const uint64_t nb = ceil_div(w, b) * ceil_div(h, b);
-    const uint64_t hdr = 24 + ceil_div(nb, 8);
-    // re-derive the winner's per-block choice, then place and emit
-    block_cost_kernel<<<dim3((unsigned)nb, 2), dim3(b * b >= 4 * kCostThreads ? kCostThreads : 64), 0, st>>>(
-        m, w, h, b, cost);
-    HC_TRY(hipGetLastError());
-    {
-        const unsigned g = (unsigned)(ceil_div(nb, 256) < 1024 ? ceil_div(nb, 256) : 1024);
-        choose_kernel<<<dim3(g), dim3(256), 0, st>>>(cost, nb, len, dir, total);
-        HC_TRY(hipGetLastError());
-    }
-    size_t tmp_bytes = 0;
-    HC_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, len, off, hipcub::Sum(), (uint64_t)hdr,
-                                             (int)nb, st));
-    void *tmp = nullptr;
-    HC_TRY(hipMalloc(&tmp, tmp_bytes + 16));
-    HC_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, tmp_bytes, len, off, hipcub::Sum(), (uint64_t)hdr,
-                                             (int)nb, st));
-    header_kernel<<<dim3((unsigned)ceil_div(hdr, 256)), dim3(256), 0, st>>>(out, w, h, b, dir, nb);
-    HC_TRY(hipGetLastError());
-    emit_kernel<<<dim3((unsigned)ceil_div(nb, 64)), dim3(64), 0, st>>>(m, w, h, b, nb, dir, off, out);
-    HC_TRY(hipGetLastError());
-    HC_TRY(hipMemcpyAsync(d_out_len, &best_len, sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    HC_TRY(hipFree(tmp));
-    HC_TRY(hipFree(cost));
-    HC_TRY(hipFree(len));
-    HC_TRY(hipFree(off));
-    HC_TRY(hipFree(dir));
-    HC_TRY(hipFree(total));
-    HC_TRY(hipStreamSynchronize(st));
-    *h_block = b;
-    return hipSuccess;
-}
-
-// transform.cpp:330-361 + headers.cpp:65-105. *d_matrix is allocated here (hipFree by caller).
-hipError_t adapt_decode(const uint8_t *sym, uint64_t nsym, uint8_t **d_matrix, uint64_t *h_len,
-                        int *h_status, hipStream_t st)
-{
-    *d_matrix = nullptr;
-    *h_len = 0;
-    if (nsym < 24) {  // headers.cpp:67-71
-        *h_status = HC_ERR_ADAPT_HEADER;
-        return hipSuccess;
-    }
-    uint8_t hdr[24];
-    HC_TRY(hipMemcpyAsync(hdr, sym, 24, hipMemcpyDeviceToHost, st));
-    HC_TRY(hipStreamSynchronize(st));
-    uint64_t f[3] = {0, 0, 0};
-    for (int k = 0; k < 3; ++k)
-        for (int i = 0; i < 8; ++i) f[k] = (f[k] << 8) | hdr[8 * k + i];
-    const uint64_t w = f[0], h = f[1], b = f[2];
-    if (b == 0) {
-        *h_status = HC_ERR_BLOCK_SIZE;
-        return hipSuccess;
-    }
-    const uint64_t nb = ceil_div(w, b) * ceil_div(h, b);
-    const uint64_t dir_bytes = ceil_div(nb, 8);
-    if (nsym - 24 < dir_bytes) {  // headers.cpp:94-98
-        *h_status = HC_ERR_ADAPT_DIRS;
-        return hipSuccess;
-    }
-    if (w != 0 && h > (1ull << 36) / w) {
-        *h_status = HC_ERR_TOO_LARGE;
-        return hipSuccess;
-    }
-    const uint64_t n = w * h;
-    uint8_t *m = nullptr;
-    uint64_t *start = nullptr;
-    int *dstat = nullptr;
-    HC_TRY(hipMalloc((void **)&m, n + 16));
-    HC_TRY(hipMalloc((void **)&start, (nb + 1) * sizeof(uint64_t)));
-    HC_TRY(hipMalloc((void **)&dstat, sizeof(int)));
-    bounds_kernel<<<1, 64, 0, st>>>(sym, nsym, w, h, b, nb, 24 + dir_bytes, start, dstat);
-    HC_TRY(hipGetLastError());
-    int status = 0;
-    HC_TRY(hipMemcpyAsync(&status, dstat, sizeof(int), hipMemcpyDeviceToHost, st));
-    HC_TRY(hipStreamSynchronize(st));
-    if (status == 0 && nb) {
-        unblock_kernel<<<dim3((unsigned)ceil_div(nb, 64)), dim3(64), 0, st>>>(sym, w, h, b, nb, sym + 24,
-                                                                              start, m);
-        HC_TRY(hipGetLastError());
-    }
-    HC_TRY(hipFree(start));
-    HC_TRY(hipFree(dstat));
-    HC_TRY(hipStreamSynchronize(st));
-    if (status != 0) {
-        (void)hipFree(m);
-        *h_status = status;
-        return hipSuccess;
-    }
-    *d_matrix = m;
-    *h_len = n;
-    *h_status = 0;
-    return hipSuccess;
+    if (b.n == 0) return hipSuccess;
+    const Ws ws = carve(work, work_bytes, b.n);
+    const DecArgs a{b.in, b.in_offs, b.in_lens, b.n, b.out, b.out_offs, b.out_caps, b.out_lens, b.status};
+    dec_plan_kernel<<<1, 1024, 0, st>>>(a, ws);
+    Batch f = b;
+    f.in_lens = ws.lens2;
+    f.out = ws.base;
+    f.out_offs = ws.sym_offs;
+    f.out_caps = ws.sym_caps;
+    f.out_lens = ws.sym_lens;
+    hipError_t e = launch_decode(f, DST_SYMBOLS, st);
+    if (e != hipSuccess) return e;
+    dec_header_kernel<<<1, 1024, 0, st>>>(a, ws);
+    bounds_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    unblock_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    chunk_sum_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    chunk_scan_kernel<<<b.n < kGrid ? b.n : kGrid, 64, 0, st>>>(a, ws);
+    undiff_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    dec_final_kernel<<<(b.n + 255) / 256, 256, 0, st>>>(a, ws);
+    return hipGetLastError();
 }
 
 }  // namespace hc

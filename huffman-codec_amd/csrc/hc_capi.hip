@@ -41,9 +41,9 @@ bool aligned4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0
 uint64_t max_symbols(uint64_t n, int use_adapt)
 {
     if (!use_adapt) return n + n / 3 + 2;
-    uint64_t b = 0;
-    (void)hc::adapt_bound(n, 8, &b);
-    return b;
+    // adaptive stream: header 24 + one bit per block, MNP-5 of a block of L bytes <= 4L/3 + 1,
+    // blocks <= n / 16 (W, H >= 8)
+    return n + n / 3 + n / 16 + n / 128 + 64;
 }
 
 // One stream through a batch launch of size 1. Per-stream scalars live in a small device
@@ -77,6 +77,36 @@ int run_single(bool encode, int mode, const uint8_t *d_in, uint64_t in_len, uint
     return HC_OK;
 }
 
+// One matrix / stream through the batched adaptive kernels (a batch of 1 with its workspace).
+int run_adapt_single(bool encode, const uint8_t *d_in, uint64_t in_len, uint64_t width, uint32_t flags,
+                     uint8_t *d_out, uint64_t out_cap, uint64_t *out_len, int *status, hipStream_t st)
+{
+    DevBuf meta, work;
+    HC_CK(meta.alloc(8 * sizeof(uint64_t)));
+    uint64_t h[8] = {0, in_len, width, 0, out_cap, 0, 0, 0};
+    HC_CK(hipMemcpyAsync(meta.p, h, sizeof(h), hipMemcpyHostToDevice, st));
+    uint64_t *m = meta.as<uint64_t>();
+    Batch b;
+    b.in = d_in;
+    b.in_offs = m + 0;
+    b.in_lens = m + 1;
+    b.n = 1;
+    b.out = d_out;
+    b.out_offs = m + 3;
+    b.out_caps = m + 4;
+    b.out_lens = m + 5;
+    b.status = reinterpret_cast<int32_t *>(m + 6);
+    b.flags = flags;
+    const uint64_t wb = encode ? hc::adapt_encode_work_bound(in_len, 1) : hc::adapt_decode_work_bound(in_len, out_cap, 1);
+    HC_CK(work.alloc(wb));
+    HC_CK(encode ? hc::adapt_encode_batch(b, m + 2, work.p, wb, st) : hc::adapt_decode_batch(b, work.p, wb, st));
+    HC_CK(hipMemcpyAsync(h, meta.p, sizeof(h), hipMemcpyDeviceToHost, st));
+    HC_CK(hipStreamSynchronize(st));
+    *out_len = h[5];
+    *status = (int32_t)h[6];
+    return HC_OK;
+}
+
 int compress_impl(const uint8_t *in, uint64_t n, int use_diff, int use_adapt, uint64_t width,
                   std::vector<uint8_t> &res)
 {
@@ -98,21 +128,9 @@ int compress_impl(const uint8_t *in, uint64_t n, int use_diff, int use_adapt, ui
                                   dout.as<uint8_t>(), cap, 0, &len, &status, st);
         if (rc) return rc;
     } else {
-        if (use_diff) HC_CK(hc::diff_apply(din.as<uint8_t>(), n, st));  // main.cpp:62-64
-        uint64_t sb = 0;
-        (void)hc::adapt_bound(n, width, &sb);
-        DevBuf dsym, dlen;
-        HC_CK(dsym.alloc(sb));
-        HC_CK(dlen.alloc(sizeof(uint64_t)));
-        uint64_t block = 0;
-        HC_CK(hc::adapt_encode(din.as<uint8_t>(), width, height, dsym.as<uint8_t>(), dlen.as<uint64_t>(),
-                               &block, st));
-        uint64_t nsym = 0;
-        HC_CK(hipMemcpyAsync(&nsym, dlen.p, sizeof(nsym), hipMemcpyDeviceToHost, st));
-        HC_CK(hipStreamSynchronize(st));
-        const uint32_t flags = (use_diff ? HC_FLAG_DIFF : 0u) | HC_FLAG_ADAPT;
-        const int rc = run_single(true, hc::SRC_SYMBOLS, dsym.as<uint8_t>(), nsym, dout.as<uint8_t>(), cap,
-                                  flags, &len, &status, st);
+        // main.cpp:62-71: [diff] -> adaptive block RLE -> FGK, through the batched kernels
+        const int rc = run_adapt_single(true, din.as<uint8_t>(), n, width, use_diff ? HC_FLAG_DIFF : 0u,
+                                        dout.as<uint8_t>(), cap, &len, &status, st);
         if (rc) return rc;
     }
     if (status) return status;
@@ -159,24 +177,24 @@ int decompress_impl(const uint8_t *in, uint64_t n, std::vector<uint8_t> &res)
         }
         return HC_ERR_CAPACITY;
     }
-    DevBuf dsym;
-    HC_CK(dsym.alloc(count + 16));
-    const int rc = run_single(false, hc::DST_SYMBOLS, din.as<uint8_t>(), n, dsym.as<uint8_t>(), count + 16,
-                              0, &len, &status, st);
-    if (rc) return rc;
-    if (status) return status;
-    uint8_t *m = nullptr;
-    uint64_t mlen = 0;
-    int ast = 0;
-    HC_CK(hc::adapt_decode(dsym.as<uint8_t>(), count, &m, &mlen, &ast, st));
-    if (ast) return ast;
-    DevBuf dm;
-    dm.p = m;
-    if (flags & HC_FLAG_DIFF) HC_CK(hc::diff_revert(m, mlen, st));  // main.cpp:123-125
-    HC_CK(hipStreamSynchronize(st));
-    res.resize(mlen);
-    if (mlen) HC_CK(hipMemcpy(res.data(), m, mlen, hipMemcpyDeviceToHost));
-    return HC_OK;
+    // main.cpp:114-125: FGK -> adaptive block revert -> [diff revert]; the matrix size is in
+    // the adaptive header, so guess, and rerun with the size the device reports if short
+    uint64_t cap = n * 16 > (1u << 20) ? n * 16 : (1u << 20);
+    for (int pass = 0; pass < 2; ++pass) {
+        DevBuf dout;
+        HC_CK(dout.alloc(cap));
+        const int rc = run_adapt_single(false, din.as<uint8_t>(), n, 0, 0, dout.as<uint8_t>(), cap, &len, &status, st);
+        if (rc) return rc;
+        if (status == HC_ERR_CAPACITY && pass == 0) {
+            cap = len;
+            continue;
+        }
+        if (status) return status;
+        res.resize(len);
+        if (len) HC_CK(hipMemcpy(res.data(), dout.p, len, hipMemcpyDeviceToHost));
+        return HC_OK;
+    }
+    return HC_ERR_CAPACITY;
 }
 
 }  // namespace
@@ -257,6 +275,45 @@ int hc_decompress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64
     if (!aligned4(in) || !aligned4(out)) return HC_ERR_ARG;
     Batch b{in, in_offs, in_lens, n_streams, out, out_offs, out_caps, out_lens, status, 0};
     const hipError_t e = hc::launch_decode(b, hc::DST_RAW, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? HC_OK : HC_ERR_DEVICE;
+}
+
+uint64_t hc_adapt_compress_work_bound(uint64_t total_in_bytes, uint32_t n_streams)
+{
+    return hc::adapt_encode_work_bound(total_in_bytes, n_streams);
+}
+
+uint64_t hc_adapt_decompress_work_bound(uint64_t total_in_bytes, uint64_t total_out_bytes, uint32_t n_streams)
+{
+    return hc::adapt_decode_work_bound(total_in_bytes, total_out_bytes, n_streams);
+}
+
+int hc_compress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                            const uint64_t *widths, uint32_t n_streams, uint32_t flags, uint8_t *out,
+                            const uint64_t *out_offs, const uint64_t *out_caps, uint64_t *out_lens,
+                            int32_t *status, void *work, uint64_t work_bytes, void *stream)
+{
+    if (n_streams == 0) return HC_OK;
+    if (!in || !in_offs || !in_lens || !widths || !out || !out_offs || !out_caps || !out_lens || !status || !work)
+        return HC_ERR_ARG;
+    if (flags & ~(HC_FLAG_DIFF | HC_FLAG_ADAPT)) return HC_ERR_ARG;
+    if (!aligned4(in) || !aligned4(out) || (reinterpret_cast<uintptr_t>(work) & 15u)) return HC_ERR_ARG;
+    Batch b{in, in_offs, in_lens, n_streams, out, out_offs, out_caps, out_lens, status, flags & HC_FLAG_DIFF};
+    const hipError_t e = hc::adapt_encode_batch(b, widths, work, work_bytes, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? HC_OK : HC_ERR_DEVICE;
+}
+
+int hc_decompress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                              uint32_t n_streams, uint8_t *out, const uint64_t *out_offs,
+                              const uint64_t *out_caps, uint64_t *out_lens, int32_t *status, void *work,
+                              uint64_t work_bytes, void *stream)
+{
+    if (n_streams == 0) return HC_OK;
+    if (!in || !in_offs || !in_lens || !out || !out_offs || !out_caps || !out_lens || !status || !work)
+        return HC_ERR_ARG;
+    if (!aligned4(in) || (reinterpret_cast<uintptr_t>(work) & 15u)) return HC_ERR_ARG;
+    Batch b{in, in_offs, in_lens, n_streams, out, out_offs, out_caps, out_lens, status, 0};
+    const hipError_t e = hc::adapt_decode_batch(b, work, work_bytes, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? HC_OK : HC_ERR_DEVICE;
 }
 

@@ -36,17 +36,15 @@ hipError_t launch_encode(const Batch &b, EncSrc src, hipStream_t st);
 // or FGK decode to the symbol stream
 hipError_t launch_decode(const Batch &b, DecDst dst, hipStream_t st);
 
-// adaptive block RLE (hc_adapt.hip); single matrix per call
-struct AdaptPlan;
-hipError_t adapt_encode(const uint8_t *d_matrix, uint64_t width, uint64_t height, uint8_t *d_out,
-                        uint64_t *d_out_len, uint64_t *h_block, hipStream_t st);
-hipError_t adapt_bound(uint64_t n, uint64_t width, uint64_t *bytes);
-// symbols -> matrix. Returns status via *h_status (host, synchronous).
-hipError_t adapt_decode(const uint8_t *d_sym, uint64_t nsym, uint8_t **d_matrix, uint64_t *h_len,
-                        int *h_status, hipStream_t st);
-
-// elementwise helpers (hc_adapt.hip)
-hipError_t diff_apply(uint8_t *d, uint64_t n, hipStream_t st);
-hipError_t diff_revert(uint8_t *d, uint64_t n, hipStream_t st);
+// adaptive block RLE (hc_adapt.hip), batched: device pointers as in Batch, asynchronous on st.
+// Encode: matrix i = in[in_offs[i] ..) of in_lens[i] bytes and width widths[i]; flags
+// HC_FLAG_DIFF or 0; the whole -a stream (FGK included) lands in out. Decode: adaptive streams
+// -> matrices (diff revert from each stream's flags byte). `work` (16-byte aligned) must hold
+// the bound below; streams that do not fit report HC_ERR_CAPACITY.
+hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work, uint64_t work_bytes,
+                              hipStream_t st);
+hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, hipStream_t st);
+uint64_t adapt_encode_work_bound(uint64_t total_in, uint32_t n);
+uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t n);
 
 }  // namespace hc

@@ -81,6 +81,13 @@ def lib():
     L.hc_decompress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
     L.hc_compress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp]
     L.hc_decompress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, vp, vp, vp, vp]
+    L.hc_adapt_compress_work_bound.argtypes = [u64, ctypes.c_uint32]
+    L.hc_adapt_compress_work_bound.restype = u64
+    L.hc_adapt_decompress_work_bound.argtypes = [u64, u64, ctypes.c_uint32]
+    L.hc_adapt_decompress_work_bound.restype = u64
+    L.hc_compress_adapt_batch.argtypes = [vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, vp,
+                                          vp, u64, vp]
+    L.hc_decompress_adapt_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp, u64, vp]
     L.hc_pack_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp]
     L.hc_version.restype = ctypes.c_char_p
     L.hc_device_ok.restype = ctypes.c_int
@@ -177,6 +184,42 @@ def decompress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, s
                                    _stream_handle(stream))
     if rc:
         raise HCodecError(f"hc_decompress_batch failed: {rc}")
+
+
+def _work(nbytes, device):
+    import torch
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def compress_adapt_batch(inp, in_offs, in_lens, widths, out, out_offs, out_caps, out_lens, status,
+                         use_diff=False, stream=None, work=None):
+    """hc_compress_adapt_batch (-a, optionally -m) on CUDA tensors; widths: int64 per matrix.
+    The workspace is allocated here unless given (uint8 CUDA tensor)."""
+    n = _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status)
+    _check_batch(inp, in_offs, widths, out, out_offs, out_caps, out_lens, status)
+    if work is None:
+        work = _work(lib().hc_adapt_compress_work_bound(int(in_lens.sum()), n), inp.device)
+    rc = lib().hc_compress_adapt_batch(_dp(inp), _dp(in_offs), _dp(in_lens), _dp(widths), n,
+                                       HC_FLAG_DIFF if use_diff else 0, _dp(out), _dp(out_offs), _dp(out_caps),
+                                       _dp(out_lens), _dp(status), _dp(work), work.numel(),
+                                       _stream_handle(stream))
+    if rc:
+        raise HCodecError(f"hc_compress_adapt_batch failed: {rc}")
+    return work
+
+
+def decompress_adapt_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status, stream=None,
+                           work=None):
+    """hc_decompress_adapt_batch on CUDA tensors (adaptive streams -> matrices)."""
+    n = _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status)
+    if work is None:
+        work = _work(lib().hc_adapt_decompress_work_bound(int(in_lens.sum()), int(out_caps.sum()), n), inp.device)
+    rc = lib().hc_decompress_adapt_batch(_dp(inp), _dp(in_offs), _dp(in_lens), n, _dp(out), _dp(out_offs),
+                                         _dp(out_caps), _dp(out_lens), _dp(status), _dp(work), work.numel(),
+                                         _stream_handle(stream))
+    if rc:
+        raise HCodecError(f"hc_decompress_adapt_batch failed: {rc}")
+    return work
 
 
 def pack_batch(inp, in_offs, lens, out, out_offs, stream=None):

@@ -83,19 +83,47 @@ void hc_free(void *p);
  * ------------------------------------------------------------------------------------- */
 
 /* Compress n_streams raw streams: [diff model] -> MNP-5 RLE -> FGK -> header, fused in one
- * kernel (one stream per wavefront). flags: 0 or HC_FLAG_DIFF (adaptive streams go through
- * hc_compress). Capacity per stream: hc_compress_bound(in_len, 0) always suffices. */
+ * kernel (one stream per wavefront). flags: 0 or HC_FLAG_DIFF (adaptive streams: the batched
+ * adaptive API below). Capacity per stream: hc_compress_bound(in_len, 0) always suffices. */
 int hc_compress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
                       uint32_t n_streams, uint32_t flags, uint8_t *out, const uint64_t *out_offs,
                       const uint64_t *out_caps, uint64_t *out_lens, int32_t *status,
                       void *stream);
 
 /* Decompress n_streams encoded streams (non-adaptive: a stream whose flags byte has bit 6 set
- * gets HC_ERR_UNSUPPORTED here; use hc_decompress). FGK -> RLE revert -> [diff revert], fused. */
+ * gets HC_ERR_UNSUPPORTED here; use hc_decompress_adapt_batch). FGK -> RLE revert -> [diff revert], fused. */
 int hc_decompress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
                         uint32_t n_streams, uint8_t *out, const uint64_t *out_offs,
                         const uint64_t *out_caps, uint64_t *out_lens, int32_t *status,
                         void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Batched adaptive block RLE (-a) — many W x H matrices per call, asynchronous on `stream`,
+ * DEVICE pointers as in the batched API above. huffCompress(ifs, useDiff, true, width)
+ * (main.cpp:39-87) for every matrix i = in[in_offs[i] .. +in_lens[i]) of width widths[i]:
+ * [diff model] -> adaptive block RLE (transform.cpp:294-328: block-size search, per-block
+ * scan order, header) -> FGK -> <u64 count><flags 0x40 | diff> header. Per-stream status:
+ * HC_OK, HC_ERR_WIDTH (width 0), HC_ERR_MATRIX_SIZE, HC_ERR_DIMS, HC_ERR_CAPACITY,
+ * HC_ERR_UNSUPPORTED. `work` is device scratch of work_bytes (16-byte aligned), at least
+ * hc_adapt_compress_work_bound(sum of in_lens, n_streams); out capacity per stream:
+ * hc_compress_bound(in_len, 1) always suffices.
+ * ------------------------------------------------------------------------------------- */
+uint64_t hc_adapt_compress_work_bound(uint64_t total_in_bytes, uint32_t n_streams);
+int hc_compress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                            const uint64_t *widths, uint32_t n_streams, uint32_t flags, uint8_t *out,
+                            const uint64_t *out_offs, const uint64_t *out_caps, uint64_t *out_lens,
+                            int32_t *status, void *work, uint64_t work_bytes, void *stream);
+
+/* huffDecompress (main.cpp:90-128) of adaptive streams (flags bit 6 set; others get
+ * HC_ERR_UNSUPPORTED): FGK -> adaptive block revert (transform.cpp:330-361) -> [diff revert].
+ * Status: HC_OK, 8, 9, 10, 11, 13, 14, 15, HC_ERR_CAPACITY (out_lens[i] = W * H needed),
+ * HC_ERR_BLOCK_SIZE, HC_ERR_TOO_LARGE, HC_ERR_UNSUPPORTED. `work`: at least
+ * hc_adapt_decompress_work_bound(sum of in_lens, sum of out_caps, n_streams) bytes. */
+uint64_t hc_adapt_decompress_work_bound(uint64_t total_in_bytes, uint64_t total_out_bytes, uint32_t n_streams);
+int hc_decompress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                              uint32_t n_streams, uint8_t *out, const uint64_t *out_offs,
+                              const uint64_t *out_caps, uint64_t *out_lens, int32_t *status, void *work,
+                              uint64_t work_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Host-buffer batch API — many independent streams in HOST memory (e.g. files read by the

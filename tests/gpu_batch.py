@@ -49,3 +49,25 @@ def decompress_batch(hc, torch, encs, caps):
     hc.decompress_batch(din, ioffs, ilens, dout, ooffs, ocaps, olens, st)
     torch.cuda.synchronize()
     return st.cpu().tolist(), unpack(torch, dout, ooffs, olens), olens.cpu().tolist()
+
+
+def compress_adapt_batch(hc, torch, raws, widths, use_diff, caps=None):
+    din, ioffs, ilens, _ = pack(torch, raws)
+    caps = caps if caps is not None else [hc.compress_bound(len(r), True) for r in raws]
+    dout, ooffs, _, ocaps = pack(torch, [b""] * len(raws), caps)
+    w = torch.tensor(list(widths), dtype=torch.int64, device="cuda")
+    olens = torch.zeros(len(raws), dtype=torch.int64, device="cuda")
+    st = torch.full((len(raws),), -1, dtype=torch.int32, device="cuda")
+    hc.compress_adapt_batch(din, ioffs, ilens, w, dout, ooffs, ocaps, olens, st, use_diff=use_diff)
+    torch.cuda.synchronize()
+    return st.cpu().tolist(), unpack(torch, dout, ooffs, olens), olens.cpu().tolist()
+
+
+def decompress_adapt_batch(hc, torch, encs, caps):
+    din, ioffs, ilens, _ = pack(torch, encs)
+    dout, ooffs, _, ocaps = pack(torch, [b""] * len(encs), caps)
+    olens = torch.zeros(len(encs), dtype=torch.int64, device="cuda")
+    st = torch.full((len(encs),), -1, dtype=torch.int32, device="cuda")
+    hc.decompress_adapt_batch(din, ioffs, ilens, dout, ooffs, ocaps, olens, st)
+    torch.cuda.synchronize()
+    return st.cpu().tolist(), unpack(torch, dout, ooffs, olens), olens.cpu().tolist()
