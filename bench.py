@@ -255,30 +255,79 @@ def config_batch(torch, hc, dev, stream, name, what, kind, S, use_diff, steps, d
     return out, bad
 
 
-def config_c4(torch, hc, digests):
-    """C4: -c -a -w 4096 (and -c -a -m) on one 4096x4096 photo matrix, single-buffer API (host
-    buffers: the wall time includes the H2D / D2H copies)"""
-    dev = torch.device("cuda", 0)
-    buf = torch.empty(4096 * 4096, dtype=torch.uint8, device=dev)
-    hc.synth_batch("photo", 0, 1, 4096, 4096, buf, 0)
-    torch.cuda.synchronize()
-    raw = buf.cpu().numpy().tobytes()
-    del buf
-    res, bad = {}, 0
-    e = digests["synthetic_4096"]["photo_0"]
-    for mode, d in (("ca", False), ("cma", True)):
-        t0 = time.perf_counter()
-        st, out = hc.compress(raw, d, True, 4096)
-        t1 = time.perf_counter()
-        st2, back = hc.decompress(out)
-        t2 = time.perf_counter()
-        ident = st == 0 and (len(out), sha(out)) == (e[mode]["len"], e[mode]["sha256"])
-        rt = st2 == 0 and back == raw
-        bad += (0 if ident else 1) + (0 if rt else 1)
-        res[mode] = {"what": f"4096x4096 photo {'-c -a -m' if d else '-c -a'} -w 4096, single-buffer API incl. PCIe",
-                     "encode_s": round(t1 - t0, 4), "decode_s": round(t2 - t1, 4), "bytes": len(out),
-                     "reference_digest_identical": ident, "round_trip_exact": rt}
-    return res, bad
+class AdaptBatch:
+    """S synthetic side x side matrices resident in HBM, coded with -c -a [-m] through the batched
+    adaptive API (hc_compress_adapt_batch / hc_decompress_adapt_batch), workspaces preallocated"""
+
+    def __init__(self, torch, hc, dev, kind, S, use_diff, side):
+        self.torch, self.hc, self.dev, self.S, self.use_diff = torch, hc, dev, S, use_diff
+        self.N = side * side
+        N = self.N
+        self.cap = 2 * N + 4096 if side <= 512 else (hc.compress_bound(N, True) + 255) // 256 * 256
+        self.raw = torch.empty(S * N, dtype=torch.uint8, device=dev)
+        hc.synth_batch(kind, 0, S, side, side, self.raw, N)
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.offs = torch.arange(S, **i64) * N
+        self.lens = torch.full((S,), N, **i64)
+        self.widths = torch.full((S,), side, **i64)
+        self.enc = torch.empty(S * self.cap, dtype=torch.uint8, device=dev)
+        self.eoffs = torch.arange(S, **i64) * self.cap
+        self.ecaps = torch.full((S,), self.cap, **i64)
+        self.elens = torch.zeros(S, **i64)
+        self.est = torch.zeros(S, dtype=torch.int32, device=dev)
+        self.back = torch.empty_like(self.raw)
+        self.blens = torch.zeros_like(self.lens)
+        self.bst = torch.zeros_like(self.est)
+        L = hc.lib()
+        self.wenc = torch.empty(int(L.hc_adapt_compress_work_bound(S * N, S)), dtype=torch.uint8, device=dev)
+        # the decode workspace is sized from the encoded lengths: one untimed encode first
+        hc.compress_adapt_batch(self.raw, self.offs, self.lens, self.widths, self.enc, self.eoffs, self.ecaps,
+                                self.elens, self.est, use_diff=use_diff, work=self.wenc)
+        torch.cuda.synchronize(dev)
+        self.wdec = torch.empty(int(L.hc_adapt_decompress_work_bound(int(self.elens.sum()), S * N, S)),
+                                dtype=torch.uint8, device=dev)
+
+    def step(self, stream, ev=None):
+        hc = self.hc
+        if ev is not None:
+            ev[0].record(stream)
+        hc.compress_adapt_batch(self.raw, self.offs, self.lens, self.widths, self.enc, self.eoffs, self.ecaps,
+                                self.elens, self.est, use_diff=self.use_diff, stream=stream, work=self.wenc)
+        if ev is not None:
+            ev[1].record(stream)
+        hc.decompress_adapt_batch(self.enc, self.eoffs, self.elens, self.back, self.offs, self.lens, self.blens,
+                                  self.bst, stream=stream, work=self.wdec)
+        if ev is not None:
+            ev[2].record(stream)
+
+    bad = Batch.bad
+    encoded = Batch.encoded
+
+
+def config_adapt(torch, hc, dev, stream, what, S, side, use_diff, steps, digests):
+    """-c -a [-m] on S side x side photo matrices, device-resident, batched adaptive API; checked
+    against the reference's digests (512x512 k = 0..3, or the 4096x4096 matrix) and by round trip"""
+    b = AdaptBatch(torch, hc, dev, "photo", S, use_diff, side)
+    wall, enc_ms, dec_ms = timed(torch, b, stream, steps, 1)
+    bad = b.bad()
+    mode = "cma" if use_diff else "ca"
+    ok = True
+    for k in range(min(S, 4)):
+        want = digests["synthetic"][f"photo_{k}"][mode] if side == 512 else digests["synthetic_4096"]["photo_0"][mode]
+        got = b.encoded(k)
+        ok &= (len(got), sha(got)) == (want["len"], want["sha256"])
+    bad += 0 if ok else 1
+    enc_bytes = int(b.elens.sum())
+    out = {"what": what, "streams": S, "mode": "-c -a -m" if use_diff else "-c -a", "kind": "photo",
+           "side": side, "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+           "GiBps": round(S * b.N / ((enc_ms + dec_ms) * 1e-3) / 2**30, 4),
+           "encode_GiBps": round(S * b.N / (enc_ms * 1e-3) / 2**30, 4),
+           "decode_GiBps": round(S * b.N / (dec_ms * 1e-3) / 2**30, 4),
+           "bits_per_byte": round(enc_bytes * 8 / (S * b.N), 4), "round_trip_exact": b.bad() == 0,
+           "reference_digests_identical": bool(ok)}
+    del b
+    torch.cuda.empty_cache()
+    return out, bad
 
 
 def run_configs(torch, hc, dev, stream, only):
@@ -296,8 +345,16 @@ def run_configs(torch, hc, dev, stream, only):
             continue
         res[name], b = config_batch(torch, hc, dev, stream, name, what, kind, S, d, steps, digests)
         bad += b
-    if not only or "C4" in only:
-        res["C4"], b = config_c4(torch, hc, digests)
+    aplan = [
+        ("C4", "1 x 4096x4096 photo -c -a -w 4096 (one matrix: one FGK wavefront), device-resident", 1, 4096, False, 2),
+        ("C4m", "1 x 4096x4096 photo -c -a -m -w 4096, device-resident", 1, 4096, True, 2),
+        ("A512", "8192 x 512x512 photo -c -a -m (the reference's best-bpc mode), batched adaptive API", 8192, 512,
+         True, 3),
+    ]
+    for name, what, S, side, d, steps in aplan:
+        if only and name not in only:
+            continue
+        res[name], b = config_adapt(torch, hc, dev, stream, what, S, side, d, steps, digests)
         bad += b
     return res, bad
 

@@ -62,6 +62,10 @@ struct AMeta {
     uint32_t nc, diff;
     int32_t status;
     uint32_t best;                   // encode: the chosen candidate
+    uint32_t mode;                   // decode: 0 tile groups (B = 8..128, power of 2), 1 one entry
+                                     // per block (B >= 256, power of 2), 2 K-block groups (other B)
+    uint32_t pad2;
+    uint64_t tiles;                  // decode: tiles (mode 0)
 };
 
 // workspace: [meta n][idx0 n+1][idx1 n+1][idx2 n+1][idx3 n+1][sym_offs n][sym_lens n][sym_caps n]
@@ -115,6 +119,38 @@ Ws carve(void *work, uint64_t bytes, uint32_t n)
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint64_t lanes_below(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// DPP data movement (gfx9 wave64): value of lane l - s within the 16-lane row (row_shr), of the
+// row's lane 15 / the wave's lane 31 (row_bcast 15 / 31, rows picked by the row mask), of lane
+// l - 1 across the wave (wave_shr 1). Lanes without a source get `id`.
+template <int kCtrl, int kRows = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t v, uint32_t id)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, kCtrl, kRows, 0xF, false);
+}
+
+// inclusive wave scan with an associative op(later, earlier) and its identity: rows by row_shr
+// 1, 2, 4, 8, then rows 1 and 3 take lane 15 / 47, rows 2 and 3 lane 31 (no LDS traffic)
+template <class Op>
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v, uint32_t id, Op op)
+{
+    v = op(v, dpp<0x111>(v, id));
+    v = op(v, dpp<0x112>(v, id));
+    v = op(v, dpp<0x114>(v, id));
+    v = op(v, dpp<0x118>(v, id));
+    v = op(v, dpp<0x142, 0xA>(v, id));
+    v = op(v, dpp<0x143, 0xC>(v, id));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_incl(uint32_t v)
+{
+    return wave_scan(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+__device__ __forceinline__ uint32_t lane_shr1(uint32_t v, uint32_t id) { return dpp<0x138>(v, id); }
+__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
 
 // index i with pre[i] <= t < pre[i + 1] (pre[0] = 0, pre[n] = total, t < total)
 __device__ __forceinline__ uint32_t find_item(const uint64_t *pre, uint32_t n, uint64_t t)
@@ -230,14 +266,34 @@ __device__ __forceinline__ Seg seg_join(const Seg &x, const Seg &y)
 // cost of a whole block scan (its first bit is 0: the block starts a run)
 __device__ __forceinline__ uint32_t seg_cost(const Seg &s) { return s.n ? s.mid + run_cost(s.tail) + 1 : 0u; }
 
-__device__ __forceinline__ Seg seg_shfl_down(const Seg &s, uint32_t d)
+template <int kCtrl>
+__device__ __forceinline__ Seg seg_dpp(const Seg &s)
 {
     Seg r;
-    r.n = __shfl_down(s.n, d, 64);
-    r.lead = __shfl_down(s.lead, d, 64);
-    r.tail = __shfl_down(s.tail, d, 64);
-    r.mid = __shfl_down(s.mid, d, 64);
+    r.n = dpp<kCtrl>(s.n, 0u);
+    r.lead = dpp<kCtrl>(s.lead, 0u);
+    r.tail = dpp<kCtrl>(s.tail, 0u);
+    r.mid = dpp<kCtrl>(s.mid, 0u);
     return r;
+}
+
+// the Seg of lane l + d (d a power of two): DPP row_shl inside 16-lane rows, else a permute
+__device__ __forceinline__ Seg seg_shfl_down(const Seg &s, uint32_t d)
+{
+    switch (d) {
+    case 1: return seg_dpp<0x101>(s);
+    case 2: return seg_dpp<0x102>(s);
+    case 4: return seg_dpp<0x104>(s);
+    case 8: return seg_dpp<0x108>(s);
+    default: {
+        Seg r;
+        r.n = __shfl_down(s.n, d, 64);
+        r.lead = __shfl_down(s.lead, d, 64);
+        r.tail = __shfl_down(s.tail, d, 64);
+        r.mid = __shfl_down(s.mid, d, 64);
+        return r;
+    }
+    }
 }
 
 // ordered join over aligned groups of g lanes (g a power of two <= 64); lane 0 of a group ends
@@ -361,12 +417,67 @@ __device__ __forceinline__ T *at(const Ws &ws, uint64_t off)
     return reinterpret_cast<T *>(ws.base + off);
 }
 
+// LDS image of a tile: row r <-> y = ty0 + r - 1 (row 0: the row above the tile), byte c <->
+// x = tx0 + c - 4 (c = 3: the column left of the tile), rows kDS bytes apart.
+#define DT(r, xl) D[(r) * kDS + (xl) + 4]
+
+// one unaligned dword of the stream at byte lin (bytes outside [0, n) read as 0)
+__device__ __forceinline__ uint32_t load4(const uint8_t *m, int64_t lin, uint64_t n)
+{
+    typedef uint32_t u32u __attribute__((aligned(1)));
+    if (lin >= 0 && (uint64_t)lin + 4 <= n) return *reinterpret_cast<const u32u *>(m + lin);
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k)
+        if (lin + k >= 0 && (uint64_t)(lin + k) < n) v |= (uint32_t)m[lin + k] << (8 * k);
+    return v;
+}
+
+// bytewise a - b and a + b (mod 256 per byte)
+__device__ __forceinline__ uint32_t sub8(uint32_t a, uint32_t b)
+{
+    return ((a | 0x80808080u) - (b & 0x7F7F7F7Fu)) ^ ((a ^ ~b) & 0x80808080u);
+}
+__device__ __forceinline__ uint32_t add8(uint32_t a, uint32_t b)
+{
+    return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+}
+
+// The tile's rows ty0 - 1 .. ty0 + th - 1, bytes tx0 - 4 .. tx0 + tw - 1, as dwords (coalesced
+// along each row; all of a thread's loads issue before its LDS stores), diff model applied
+// (transform.cpp:220-229: d[k] = m[k] - m[k-1] over the linear matrix, m[-1] = 0).
+__device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64_t n, uint64_t W, uint64_t tx0,
+                                          uint64_t ty0, uint32_t tw, uint32_t th, bool diff, uint32_t tid)
+{
+    const uint32_t nd = (tw + 7) / 4, items = (th + 1) * nd;
+    constexpr int kU = 4;
+    for (uint32_t base = 0; base < items; base += 256 * kU) {
+        uint32_t v[kU], pv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t it = base + u * 256 + tid;
+            const uint32_t r = it / nd, d = it - r * nd;
+            const int64_t lin = (int64_t)(ty0 + r) * (int64_t)W - (int64_t)W + (int64_t)tx0 - 4 + 4 * (int64_t)d;
+            const bool on = it < items && (r > 0 || ty0 > 0);
+            v[u] = on ? load4(mat, lin, n) : 0u;
+            pv[u] = on && diff ? load4(mat, lin - 1, n) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t it = base + u * 256 + tid;
+            if (it < items) {
+                const uint32_t r = it / nd, d = it - r * nd;
+                *reinterpret_cast<uint32_t *>(D + r * kDS + 4 * d) = diff ? sub8(v[u], pv[u]) : v[u];
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
 {
-    __shared__ uint8_t D[(kTile + 1) * kDS];  // row r <-> y = ty0 + r - 1, column c <-> x = tx0 + c - 1
+    __shared__ uint8_t D[(kTile + 1) * kDS];  // DT(r, xl): y = ty0 + r - 1, x = tx0 + xl
     __shared__ uint64_t E[4 * kTile];         // Eh[r][2] then Ev[c][2]
     __shared__ uint32_t hv[2][256];           // candidate's block costs, h / v
-    __shared__ Seg part[4];
+    __shared__ Seg part[8];
     __shared__ uint32_t red[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[0];
@@ -382,19 +493,7 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
         const uint8_t *mat = a.in + a.in_offs[i];
         const bool diff = a.diff != 0;
         // 1. the tile plus one row above and one column to the left, diff model applied
-        //    (transform.cpp:220-229: d[k] = m[k] - m[k-1] over the linear matrix)
-        for (uint32_t r = wv; r <= th; r += 4) {
-            if (r == 0 && ty0 == 0) continue;
-            const uint64_t y = ty0 + r - 1;
-            const uint8_t *row = mat + y * W;
-            for (uint32_t c = lane; c <= tw; c += 64) {
-                if (c == 0 && tx0 == 0) continue;
-                const uint64_t x = tx0 + c - 1;
-                uint32_t v = row[x];
-                if (diff) v -= (x | y) ? row[(int64_t)x - 1] : 0u;
-                D[r * kDS + c] = (uint8_t)v;
-            }
-        }
+        load_tile(D, mat, M.w * M.h, W, tx0, ty0, tw, th, diff, tid);
         __syncthreads();
         // 2. Eh[r][k] bit j: x = tx0 + 64k + j equals x - 1 (row ty0 + r); Ev[c][k] bit j: y = ty0 +
         //    64k + j equals y - 1 (column tx0 + c). One ballot per word; lane k keeps word k.
@@ -409,10 +508,10 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                     if (q < nh) {
                         const uint32_t rr = q >> 1, col = 64 * (q & 1) + lane;
                         e = col < tw && tx0 + col > 0 &&
-                            D[(rr + 1) * kDS + col + 1] == D[(rr + 1) * kDS + col];
+                            DT(rr + 1, col) == DT(rr + 1, (int)col - 1);
                     } else {
                         const uint32_t cc = (q - nh) >> 1, row = 64 * ((q - nh) & 1) + lane;
-                        e = row < th && ty0 + row > 0 && D[(row + 1) * kDS + cc + 1] == D[row * kDS + cc + 1];
+                        e = row < th && ty0 + row > 0 && DT(row + 1, cc) == DT(row, cc);
                     }
                     const uint64_t b = ballot(e);
                     keep = lane == k ? b : keep;
@@ -431,7 +530,54 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
             const uint32_t B = 8u << c, lg = 3 + c;
             const uint32_t nbx = (tw + B - 1) >> lg, nby = (th + B - 1) >> lg;
             const uint32_t per_o = (nbx * nby) << lg, items = 2 * per_o;
-            for (uint32_t base = 0; base < items; base += 256) {
+            const bool full = (tw & (B - 1)) == 0 && (th & (B - 1)) == 0;
+            // whole blocks: one 64-element word of the block's scan per lane (64 / B block rows or
+            // columns, B = 128: half of one), first bits substituted, so a block of B = 8 is one
+            // leaf and no join; 2 (h, v) x tw x th / 64 items
+            const uint32_t lwpb = lg <= 3 ? 0u : 2 * lg - 6;  // log2 of the words per block
+            const uint32_t nwords = (tw * th) >> 6;
+            for (uint32_t base = 0; full && base < 2 * nwords; base += 256) {
+                const uint32_t it = base + tid;
+                const uint32_t o = it >= nwords, wi = it - (o ? nwords : 0u);
+                const uint32_t blk = wi >> lwpb, j = wi & ((1u << lwpb) - 1);
+                const uint32_t bx = blk % nbx, by = blk / nbx;
+                const uint32_t x0 = bx << lg, y0 = by << lg;
+                uint64_t word = 0;
+                if (it < 2 * nwords) {
+                    const uint64_t *E2 = o ? Ev : Eh;
+                    const uint32_t l0 = o ? x0 : y0, c0 = o ? y0 : x0;  // first line, offset in it
+                    if (B <= 64) {
+                        const uint32_t lpw = 64 >> lg, r0 = j * lpw;
+                        const uint64_t msk = B >= 64 ? ~0ull : (1ull << B) - 1;
+                        for (uint32_t q = 0; q < lpw; ++q) {
+                            const uint32_t r = r0 + q;
+                            uint64_t bits = (E2[2 * (l0 + r) + (c0 >> 6)] >> (c0 & 63)) & msk & ~1ull;
+                            if (r) {  // the scan's step across the line wrap (transform.cpp:66-94)
+                                const bool eq = o ? DT(y0 + 1, x0 + r) == DT(y0 + B, (int)(x0 + r) - 1)
+                                                  : DT(y0 + r + 1, x0) == DT(y0 + r, x0 + B - 1);
+                                bits |= eq;
+                            }
+                            word |= bits << (q * B);
+                        }
+                    } else {  // B = 128 (x0 = y0 = 0): word j = half j & 1 of line j >> 1
+                        const uint32_t r = j >> 1;
+                        word = E2[2 * r + (j & 1)];
+                        if ((j & 1) == 0) {
+                            word &= ~1ull;
+                            if (r) word |= o ? DT(1, r) == DT(B, (int)r - 1) : DT(r + 1, 0) == DT(r, B - 1);
+                        }
+                    }
+                }
+                Seg sg = it < 2 * nwords ? seg_leaf(word, 64) : seg_id();
+                const uint32_t G = 1u << lwpb;
+                sg = seg_group(sg, G < 64 ? G : 64u, lane);
+                if (G <= 64) {
+                    if ((lane & (G - 1)) == 0 && it < 2 * nwords) hv[o][blk] = seg_cost(sg);
+                } else if (lane == 0) {
+                    part[4 * o + wv] = sg;
+                }
+            }
+            for (uint32_t base = 0; !full && base < items; base += 256) {
                 const uint32_t it = base + tid;
                 const uint32_t o = it >= per_o, q = it - (o ? per_o : 0u);
                 const uint32_t blk = q >> lg, r = q & (B - 1);
@@ -443,12 +589,12 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                     if (o == 0 && r < sy) {  // block row r (transform.cpp:66-94, horizontal)
                         const uint32_t y = y0 + r;
                         const uint32_t first =
-                            r ? (uint32_t)(D[(y + 1) * kDS + x0 + 1] == D[y * kDS + x0 + sx]) : 0u;
+                            r ? (uint32_t)(DT(y + 1, x0) == DT(y, x0 + sx - 1)) : 0u;
                         s = seg_piece(Eh + 2 * y, x0, sx, first);
                     } else if (o == 1 && r < sx) {  // block column r (vertical)
                         const uint32_t x = x0 + r;
                         const uint32_t first =
-                            r ? (uint32_t)(D[(y0 + 1) * kDS + x + 1] == D[(y0 + sy) * kDS + x]) : 0u;
+                            r ? (uint32_t)(DT(y0 + 1, x) == DT(y0 + sy, (int)x - 1)) : 0u;
                         s = seg_piece(Ev + 2 * x, y0, sy, first);
                     }
                 }
@@ -460,7 +606,10 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                 }
             }
             __syncthreads();
-            if (B == 128 && tid < 2) hv[tid][0] = seg_cost(seg_join(part[2 * tid], part[2 * tid + 1]));
+            if (B == 128 && tid < 2)
+                hv[tid][0] = full ? seg_cost(seg_join(seg_join(part[4 * tid], part[4 * tid + 1]),
+                                                      seg_join(part[4 * tid + 2], part[4 * tid + 3])))
+                                  : seg_cost(seg_join(part[2 * tid], part[2 * tid + 1]));
             __syncthreads();
             // transform.cpp:113-123: the shorter scan, ties horizontal; word = cost | h << 31
             const uint32_t nblk = nbx * nby;
@@ -487,7 +636,7 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                                                 : seg_leaf(w[0] >> 1, tw - 1))
                                      : seg_id();
                 pc[(ty0 + tid) * ntx + tx0 / kTile] =
-                    piece_pack(s, (uint32_t)(w[0] & 1), D[(tid + 1) * kDS + 1], D[(tid + 1) * kDS + tw]);
+                    piece_pack(s, (uint32_t)(w[0] & 1), DT(tid + 1, 0), DT(tid + 1, tw - 1));
             } else if (tid >= 128 && tid - 128 < tw) {
                 const uint32_t x = tid - 128;
                 const uint64_t *w = Ev + 2 * x;
@@ -495,7 +644,7 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                                                 : seg_leaf(w[0] >> 1, th - 1))
                                      : seg_id();
                 pc[H * ntx + (tx0 + x) * nty + ty0 / kTile] =
-                    piece_pack(s, (uint32_t)(w[0] & 1), D[kDS + x + 1], D[th * kDS + x + 1]);
+                    piece_pack(s, (uint32_t)(w[0] & 1), DT(1, x), DT(th, x));
             }
         }
         __syncthreads();
@@ -644,30 +793,108 @@ __device__ __forceinline__ uint32_t div_small(uint32_t q, uint32_t d, float inv)
     return r;
 }
 
-// transform.cpp:241-279 for one block's scan per wave, 64 elements per step (model:
-// tests/adapt_cost_model.py emit_lanes)
-__global__ __launch_bounds__(256) void emit_kernel(EncArgs a, Ws ws)
+// transform.cpp:241-279 on one block's scan, by one wave, 64 elements per step (model:
+// tests/adapt_cost_model.py emit_lanes): element p's run offset o comes from a ballot of run
+// starts (carried across steps), j = o mod 258; it emits its byte for j <= 2, 255 at j = 257,
+// the count j - 2 where its run ends (3 <= j + 1 <= 257), and the block's last element is a
+// literal. Byte offsets: popcounts of two ballots. value(p) = the p-th element in scan order.
+template <class Value>
+__device__ __forceinline__ void emit_block(Value value, uint32_t L, uint8_t *out, uint32_t lane)
+{
+    const uint64_t lt = lanes_below(lane);
+    uint32_t pv = 0, po = 0;  // value and run offset of the previous step's last element
+    uint64_t q = 0;           // bytes written
+    for (uint32_t base = 0; base < L; base += 64) {
+        const uint32_t p = base + lane;
+        const bool valid = p < L;
+        const uint32_t v = valid ? value(p) : 0u;
+        const uint32_t prev = lane_shr1(v, pv);
+        const uint32_t nx = dpp<0x130>(v, base + 64 < L ? value(base + 64) : 0u);  // wave_shl 1
+        const bool start = p == 0 || v != prev;
+        const uint64_t sm = ballot(valid && start);
+        const uint64_t le = sm & (lt | (1ull << lane));
+        const uint32_t o = le ? lane - (63u - (uint32_t)__builtin_clzll(le)) : po + 1 + lane;
+        const uint32_t j = o % 258u;
+        const bool last = p + 1 == L;
+        const bool end = p + 2 == L || (p + 2 < L && nx != v);
+        uint32_t cnt = last ? 1u : (uint32_t)(j <= 2) + (uint32_t)(j == 257) + (uint32_t)(end && j >= 2 && j <= 256);
+        if (!valid) cnt = 0;
+        const uint64_t b1 = ballot(cnt >= 1), b2 = ballot(cnt == 2);
+        const uint64_t pos = q + __popcll(b1 & lt) + __popcll(b2 & lt);
+        const uint32_t first = (last || j <= 2) ? v : (j == 257 ? 255u : j - 2);
+        if (cnt >= 1) out[pos] = (uint8_t)first;
+        if (cnt == 2) out[pos + 1] = 0;
+        q += __popcll(b1) + __popcll(b2);
+        po = readlane(o, 63);
+        pv = readlane(v, 63);
+    }
+}
+
+// blocks of B <= 128: one workgroup per tile loads it once into LDS (as tile_cost_kernel
+// does), then each wave emits blocks of the tile from LDS
+__global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
+{
+    __shared__ uint8_t D[(kTile + 1) * kDS];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t ntiles = ws.ctr[0];
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t i = find_item(ws.idx[0], a.n, t);
+        const AMeta &M = ws.meta[i];
+        if (M.status || M.B > kTile) continue;  // (uniform over the workgroup)
+        const uint64_t W = M.w, H = M.h, B = M.B;
+        const uint64_t ntx = cdiv(W, kTile), local = t - ws.idx[0][i];
+        const uint64_t tx0 = (local % ntx) * kTile, ty0 = (local / ntx) * kTile;
+        const uint32_t tw = (uint32_t)(W - tx0 < kTile ? W - tx0 : kTile);
+        const uint32_t th = (uint32_t)(H - ty0 < kTile ? H - ty0 : kTile);
+        load_tile(D, a.in + a.in_offs[i], W * H, W, tx0, ty0, tw, th, a.diff != 0, tid);
+        __syncthreads();
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        const uint32_t *offw = at<uint32_t>(ws, M.cost0[M.best]);
+        const uint32_t b32 = (uint32_t)B;
+        const uint32_t nbx = (tw + b32 - 1) / b32, nby = (th + b32 - 1) / b32;
+        const uint64_t per_row = cdiv(W, B);
+        for (uint32_t b = wv; b < nbx * nby; b += 4) {
+            const uint32_t bx = b % nbx, by = b / nbx;
+            const uint32_t x0 = bx * b32, y0 = by * b32;
+            const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
+            const uint64_t k = (ty0 / B + by) * per_row + tx0 / B + bx;
+            const bool horiz = (sym[24 + k / 8] >> (7 - k % 8)) & 1;
+            const uint32_t inner = horiz ? sx : sy;
+            const float inv = 1.0f / (float)inner;
+            auto value = [&](uint32_t p) -> uint32_t {
+                const uint32_t a1 = div_small(p, inner, inv), b1 = p - a1 * inner;
+                const uint32_t xl = x0 + (horiz ? b1 : a1), yl = y0 + (horiz ? a1 : b1);
+                return DT(yl + 1, xl);
+            };
+            emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + offw[k], lane);
+        }
+        __syncthreads();
+    }
+}
+
+// blocks of B >= 256 (few per matrix): one wave per block straight from memory
+__global__ __launch_bounds__(256) void emit_big_kernel(EncArgs a, Ws ws)
 {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    const uint64_t items = ws.ctr[2];
-    const uint64_t lt = lanes_below(lane);
+    const uint64_t items = ws.ctr[1];
     for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
-        const uint32_t i = find_item(ws.idx[2], a.n, t);
+        const uint32_t i = find_item(ws.idx[1], a.n, t);
         const AMeta &M = ws.meta[i];
-        const uint64_t k = t - ws.idx[2][i];
-        if (M.status || k >= M.nb) continue;
+        if (M.status || M.B <= kTile) continue;
+        uint64_t k = t - ws.idx[1][i];
+        uint32_t c = kTileCand;
+        while (c < kCand - 1 && k >= M.nbc[c]) k -= M.nbc[c++];
+        if (c != M.best) continue;
         const uint64_t W = M.w, H = M.h, B = M.B;
         const uint64_t per_row = cdiv(W, B);
         const uint64_t x0 = (k % per_row) * B, y0 = (k / per_row) * B;
         const uint32_t sx = (uint32_t)(W - x0 < B ? W - x0 : B), sy = (uint32_t)(H - y0 < B ? H - y0 : B);
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
         const bool horiz = (sym[24 + k / 8] >> (7 - k % 8)) & 1;
-        uint8_t *out = at<uint8_t>(ws, M.sym) + M.hdr + at<uint32_t>(ws, M.cost0[M.best])[k];
         const uint8_t *mat = a.in + a.in_offs[i];
         const bool diff = a.diff != 0;
         const uint32_t inner = horiz ? sx : sy;
         const float inv = 1.0f / (float)inner;
-        const uint32_t L = sx * sy;
         auto value = [&](uint32_t p) -> uint32_t {
             const uint32_t a1 = div_small(p, inner, inv), b1 = p - a1 * inner;
             const uint64_t x = x0 + (horiz ? b1 : a1), y = y0 + (horiz ? a1 : b1);
@@ -676,34 +903,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EncArgs a, Ws ws)
             if (diff) v = (v - (lin ? mat[lin - 1] : 0u)) & 0xFFu;
             return v;
         };
-        uint32_t pv = 0, po = 0;  // value and run offset of the previous step's last element
-        uint64_t q = 0;           // bytes written
-        for (uint32_t base = 0; base < L; base += 64) {
-            const uint32_t p = base + lane;
-            const bool valid = p < L;
-            const uint32_t v = valid ? value(p) : 0u;
-            uint32_t prev = __shfl_up(v, 1, 64);
-            if (lane == 0) prev = pv;
-            uint32_t nx = __shfl_down(v, 1, 64);
-            if (lane == 63 && p + 1 < L) nx = value(p + 1);
-            const bool start = p == 0 || v != prev;
-            const uint64_t sm = ballot(valid && start);
-            const uint64_t le = sm & (lt | (1ull << lane));
-            const uint32_t o = le ? lane - (63u - (uint32_t)__builtin_clzll(le)) : po + 1 + lane;
-            const uint32_t j = o % 258u;
-            const bool last = p + 1 == L;
-            const bool end = p + 2 == L || (p + 2 < L && nx != v);
-            uint32_t cnt = last ? 1u : (uint32_t)(j <= 2) + (uint32_t)(j == 257) + (uint32_t)(end && j >= 2 && j <= 256);
-            if (!valid) cnt = 0;
-            const uint64_t b1 = ballot(cnt >= 1), b2 = ballot(cnt == 2);
-            const uint64_t pos = q + __popcll(b1 & lt) + __popcll(b2 & lt);
-            const uint32_t first = (last || j <= 2) ? v : (j == 257 ? 255u : j - 2);
-            if (cnt >= 1) out[pos] = (uint8_t)first;
-            if (cnt == 2) out[pos + 1] = 0;
-            q += __popcll(b1) + __popcll(b2);
-            po = __shfl(o, 63, 64);
-            pv = __shfl(v, 63, 64);
-        }
+        emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + at<uint32_t>(ws, M.cost0[M.best])[k], lane);
     }
 }
 
@@ -729,7 +929,9 @@ struct DecArgs {
     int32_t *status;
 };
 
-__device__ __forceinline__ uint64_t group_entries_bound(uint64_t cap) { return cap / 256 + 2; }
+// u32 block-start entries per stream: mode 0 ceil(H/B) * ceil(W/128) <= cap/8 + cap/128 +
+// cap/1024 + 1; mode 1 far fewer; mode 2 <= 4 W H / 1024 + 1 (dec_header_kernel)
+__device__ __forceinline__ uint64_t group_entries_bound(uint64_t cap) { return cap / 7 + 16; }
 
 // symbols the FGK stage may write: the count, unless the payload cannot hold it (the first symbol
 // takes >= 8 bits, every later one >= 1), which the FGK decoder reports as 9 without writing
@@ -750,7 +952,7 @@ __global__ __launch_bounds__(1024) void dec_plan_kernel(DecArgs a, Ws ws)
             for (int b = 7; b >= 0; --b) count = count << 8 | p[b];
         const bool ok = len >= 9 && (p[8] & HC_FLAG_ADAPT);
         const uint64_t oc = a.out_caps[i];
-        v[0] = ok ? align_up(sym_cap(count, len) + 64, 16) + align_up(8 * group_entries_bound(oc) + oc / kChunk + 16, 16)
+        v[0] = ok ? align_up(sym_cap(count, len) + 64, 16) + align_up(4 * group_entries_bound(oc) + oc / kChunk + 16, 16)
                   : 0;
     };
     auto put = [&](uint32_t i, const uint64_t *base) {
@@ -769,7 +971,7 @@ __global__ __launch_bounds__(1024) void dec_plan_kernel(DecArgs a, Ws ws)
             for (int b = 7; b >= 0; --b) count = count << 8 | p[b];
         const uint64_t cap = m.status ? 0 : sym_cap(count, len);
         m.starts = m.slab + align_up(cap + 64, 16);
-        m.csum = m.starts + 8 * group_entries_bound(a.out_caps[i]);
+        m.csum = m.starts + 4 * group_entries_bound(a.out_caps[i]);
         ws.sym_offs[i] = m.sym;
         ws.sym_caps[i] = cap;
         ws.sym_lens[i] = 0;
@@ -821,10 +1023,24 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
             a.out_lens[i] = w * h;
             return;
         }
-        const uint64_t bx = b < w ? b : w, by = b < h ? b : h;
-        const uint64_t area = bx * by;
-        m.K = area >= kGroupBytes ? 1 : cdiv(kGroupBytes, area ? area : 1);
-        m.groups = cdiv(nb, m.K);
+        const bool pow2 = (b & (b - 1)) == 0;
+        m.tiles = 0;
+        if (pow2 && b >= 8 && b <= kTile) {  // groups = the block rows of a tile
+            m.mode = 0;
+            m.K = kTile / b;
+            m.groups = 0;
+            m.tiles = cdiv(w, kTile) * cdiv(h, kTile);
+        } else if (pow2 && b > kTile) {
+            m.mode = 1;
+            m.K = 1;
+            m.groups = nb;
+        } else {  // any other block size (a forged header): groups of >= 1024 bytes
+            const uint64_t bx = b < w ? b : w, by = b < h ? b : h;
+            const uint64_t area = bx * by;
+            m.mode = 2;
+            m.K = area >= kGroupBytes ? 1 : cdiv(kGroupBytes, area ? area : 1);
+            m.groups = cdiv(nb, m.K);
+        }
         m.chunks = m.diff ? cdiv(w * h, kChunk) : 0;
     };
     for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) parse(i);
@@ -832,19 +1048,20 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
     auto need = [&](uint32_t i, uint64_t *v) {
         v[0] = ws.meta[i].status ? 0 : ws.meta[i].groups;
         v[1] = ws.meta[i].status ? 0 : ws.meta[i].chunks;
-        v[2] = ws.meta[i].status ? 0 : 1;
+        v[2] = ws.meta[i].status ? 0 : ws.meta[i].tiles;
     };
     auto put = [&](uint32_t i, const uint64_t *base) {
         ws.idx[0][i] = base[0];
         ws.idx[1][i] = base[1];
+        ws.idx[2][i] = base[2];
     };
     __shared__ uint64_t tot[3];
     wg_scan<3>(a.n, need, put, tot);
     if (threadIdx.x == 0) {
-        ws.idx[0][a.n] = tot[0];
-        ws.idx[1][a.n] = tot[1];
-        ws.ctr[0] = tot[0];
-        ws.ctr[1] = tot[1];
+        for (int k = 0; k < 3; ++k) {
+            ws.idx[k][a.n] = tot[k];
+            ws.ctr[k] = tot[k];
+        }
     }
 }
 
@@ -852,16 +1069,20 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
 // next symbol is a count): a literal equal to the previous symbol moves r -> r + 1, another one
 // r -> 1, a count 3 -> 0; from 0 both give 1, so the symbol before a block start never matters.
 // Transition functions as 4 x 2-bit tables, composed by wave scans.
-constexpr uint32_t kFsmEq = 1u | 2u << 2 | 3u << 4;  // 0->1 1->2 2->3 3->0
-constexpr uint32_t kFsmNe = 1u | 1u << 2 | 1u << 4;  // 0->1 1->1 2->1 3->0
-constexpr uint32_t kFsmId = 0u | 1u << 2 | 2u << 4 | 3u << 6;
+// A transition function is a 4-byte table (byte x = the state x goes to); g after f is one
+// v_perm_b32 (the bytes of g picked by the bytes of f).
+constexpr uint32_t kFsmEq = 0x00030201u;  // 0->1 1->2 2->3 3->0
+constexpr uint32_t kFsmNe = 0x00010101u;  // 0->1 1->1 2->1 3->0
+constexpr uint32_t kFsmId = 0x03020100u;
 
 __device__ __forceinline__ uint32_t fsm_then(uint32_t g, uint32_t f)  // x -> g(f(x))
 {
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t x = 0; x < 4; ++x) h |= ((g >> (2 * ((f >> (2 * x)) & 3u))) & 3u) << (2 * x);
-    return h;
+    return __builtin_amdgcn_perm(0u, g, f);
+}
+__device__ __forceinline__ uint32_t fsm_at(uint32_t f, uint32_t x) { return (f >> (8 * x)) & 0xFFu; }
+__device__ __forceinline__ uint32_t fsm_scan(uint32_t f)
+{
+    return wave_scan(f, kFsmId, [](uint32_t later, uint32_t earlier) { return fsm_then(later, earlier); });
 }
 
 __device__ __forceinline__ uint32_t block_size(const AMeta &m, uint64_t k, uint64_t *x0, uint64_t *y0,
@@ -889,13 +1110,22 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
         AMeta &M = ws.meta[i];
         if (M.status) continue;
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
-        uint64_t *starts = at<uint64_t>(ws, M.starts);
-        const uint64_t nsym = M.count, nb = M.nb, K = M.K;
+        uint32_t *starts = at<uint32_t>(ws, M.starts);
+        const uint64_t per_row = cdiv(M.w, M.B), ntx = cdiv(M.w, kTile);
+        // the entry of block k (or ~0 if k starts no group)
+        auto entry = [&](uint64_t k) -> uint64_t {
+            if (M.mode == 0) {
+                const uint64_t bx = k % per_row;
+                return bx % M.K ? ~0ull : (k / per_row) * ntx + bx / M.K;
+            }
+            return k % M.K ? ~0ull : k / M.K;
+        };
+        const uint64_t nsym = M.count, nb = M.nb;
         uint64_t pos = M.hdr;
         uint64_t blk = 0, got = 0;
         uint32_t r = 0, last = 0;
         int status = 0;
-        if (lane == 0 && nb) starts[0] = pos;
+        if (lane == 0 && nb) starts[0] = (uint32_t)pos;
         uint64_t want = 0;
         if (nb) {
             uint64_t x0, y0, sx, sy;
@@ -912,7 +1142,7 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
             uint32_t x[4];
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) x[k] = 4 * lane + k < m ? sym[pos + 4 * lane + k] : 0u;
-            const uint32_t up = __shfl_up(x[3], 1, 64);
+            const uint32_t up = lane_shr1(x[3], last);
             uint32_t lo = 0;  // symbols below lo belong to blocks already closed
             bool stop = false;
             for (;;) {
@@ -920,36 +1150,27 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
 #pragma unroll
                 for (uint32_t k = 0; k < 4; ++k) {
                     const uint32_t ii = 4 * lane + k;
-                    const uint32_t p = k ? x[k - 1] : (lane ? up : last);
+                    const uint32_t p = k ? x[k - 1] : up;
                     f[k] = (ii >= lo && ii < m) ? (x[k] == p ? kFsmEq : kFsmNe) : kFsmId;
                     F = fsm_then(f[k], F);
                 }
-                uint32_t inc = F;
-                for (uint32_t off = 1; off < 64; off <<= 1) {
-                    const uint32_t g = __shfl_up(inc, off, 64);
-                    inc = lane >= off ? fsm_then(inc, g) : inc;
-                }
-                const uint32_t ex = __shfl_up(inc, 1, 64);
-                uint32_t s = ((lane ? ex : kFsmId) >> (2 * r)) & 3u;
+                const uint32_t inc = fsm_scan(F);
+                uint32_t s = fsm_at(lane_shr1(inc, kFsmId), r);
                 uint32_t len[4], tot = 0;
 #pragma unroll
                 for (uint32_t k = 0; k < 4; ++k) {
                     const uint32_t ii = 4 * lane + k;
                     len[k] = (ii >= lo && ii < m) ? (s == 3 ? x[k] : 1u) : 0u;
                     tot += len[k];
-                    s = (f[k] >> (2 * s)) & 3u;
+                    s = fsm_at(f[k], s);
                 }
-                uint32_t acc = tot;
-                for (uint32_t off = 1; off < 64; off <<= 1) {
-                    const uint32_t g = __shfl_up(acc, off, 64);
-                    acc += lane >= off ? g : 0u;
-                }
+                const uint32_t acc = wave_sum_incl(tot);
                 const uint64_t need = want - got;  // >= 1
                 const uint64_t hit = ballot((uint64_t)acc >= need);
                 if (!hit) {  // the block goes on past this step
-                    got += __shfl(acc, 63, 64);
-                    r = (__shfl(inc, 63, 64) >> (2 * r)) & 3u;
-                    last = __shfl(x[(m - 1) & 3u], (m - 1) >> 2, 64);
+                    got += readlane(acc, 63);
+                    r = fsm_at(readlane(inc, 63), r);
+                    last = readlane(x[(m - 1) & 3u], (m - 1) >> 2);
                     pos += m;
                     break;
                 }
@@ -963,8 +1184,8 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
                         cj = c;
                     }
                 }
-                j = __shfl(j, L, 64);
-                cj = __shfl(cj, L, 64);
+                j = readlane(j, L);
+                cj = readlane(cj, L);
                 if ((uint64_t)cj != need) {  // transform.cpp:178-182: a count overshoots the block
                     status = HC_ERR_BLOCK_DATA;
                     stop = true;
@@ -972,7 +1193,10 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
                 }
                 lo = j + 1;
                 ++blk;
-                if (blk < nb && blk % K == 0 && lane == 0) starts[blk / K] = pos + lo;
+                if (blk < nb && lane == 0) {
+                    const uint64_t e = entry(blk);
+                    if (e != ~0ull) starts[e] = (uint32_t)(pos + lo);
+                }
                 if (blk == nb) {
                     pos += lo;
                     break;
@@ -994,8 +1218,96 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
     }
 }
 
-// transform.cpp:162-216 for the blocks of one group per wave: revert each block's RLE from its
-// start with a fresh machine, 64 symbols per step, and scatter the bytes in scan order.
+// transform.cpp:162-187 for one block by one wave: revert its RLE from symbol `pos` with a
+// fresh machine, 64 symbols per step, handing every output byte (block-relative index q in scan
+// order, value) to place(); returns the block's end. A count repeats the literal before it.
+template <class Place>
+__device__ __forceinline__ uint64_t revert_block(const uint8_t *sym, uint64_t pos, uint64_t count, uint64_t want,
+                                                 Place place, uint32_t lane)
+{
+    uint64_t got = 0;
+    uint32_t r = 0, last = 0;
+    while (got < want && pos < count) {  // (the bounds pass proved the block whole)
+        const uint32_t xs = sym[pos + lane];
+        const uint32_t pr = lane_shr1(xs, last);
+        const uint32_t inc = fsm_scan(xs == pr ? kFsmEq : kFsmNe);
+        const uint32_t s = fsm_at(lane_shr1(inc, kFsmId), r);
+        const uint32_t len = s == 3 ? xs : 1u;
+        const uint32_t val = s == 3 ? pr : xs;
+        const uint32_t acc = wave_sum_incl(len);
+        const uint64_t need = want - got;
+        const uint64_t hit = ballot((uint64_t)acc >= need);
+        const uint32_t L = hit ? (uint32_t)__builtin_ctzll(hit) : 63u;  // last lane of this block
+        const bool mine = lane <= L;
+        const uint64_t q0 = got + acc - len;
+        if (mine)
+            for (uint32_t e = 0; e < len; ++e) place(q0 + e, val);
+        got += readlane(acc, L);
+        r = fsm_at(readlane(inc, L), r);
+        last = readlane(xs, L);
+        pos += L + 1;
+    }
+    return pos;
+}
+
+// transform.cpp:191-216 for blocks of B = 8..128 (mode 0): one workgroup per tile; each wave
+// reverts the blocks of one tile block row (one group: they follow each other in the stream)
+// into an LDS image of the tile, which then leaves as whole rows
+__global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
+{
+    __shared__ uint8_t T[kTile * kDS];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t ntiles = ws.ctr[2];
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t i = find_item(ws.idx[2], a.n, t);
+        const AMeta &M = ws.meta[i];
+        if (M.status || M.mode != 0) continue;  // (uniform over the workgroup)
+        const uint64_t W = M.w, H = M.h, B = M.B;
+        const uint64_t ntx = cdiv(W, kTile), local = t - ws.idx[2][i];
+        const uint64_t tix = local % ntx, tx0 = tix * kTile, ty0 = (local / ntx) * kTile;
+        const uint32_t tw = (uint32_t)(W - tx0 < kTile ? W - tx0 : kTile);
+        const uint32_t th = (uint32_t)(H - ty0 < kTile ? H - ty0 : kTile);
+        const uint32_t b32 = (uint32_t)B;
+        const uint32_t nbx = (tw + b32 - 1) / b32, nby = (th + b32 - 1) / b32;
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        const uint32_t *starts = at<uint32_t>(ws, M.starts);
+        const uint64_t per_row = cdiv(W, B);
+        for (uint32_t by = wv; by < nby; by += 4) {
+            const uint64_t gby = ty0 / B + by;
+            uint64_t pos = starts[gby * ntx + tix];
+            for (uint32_t bx = 0; bx < nbx; ++bx) {
+                const uint64_t k = gby * per_row + tx0 / B + bx;
+                const uint32_t x0 = bx * b32, y0 = by * b32;
+                const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
+                const bool horiz = (sym[24 + k / 8] >> (7 - k % 8)) & 1;
+                const uint32_t inner = horiz ? sx : sy;
+                const float inv = 1.0f / (float)inner;
+                auto place = [&](uint64_t q, uint32_t v) {
+                    const uint32_t a1 = div_small((uint32_t)q, inner, inv), b1 = (uint32_t)q - a1 * inner;
+                    T[(y0 + (horiz ? a1 : b1)) * kDS + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
+                };
+                pos = revert_block(sym, pos, M.count, (uint64_t)sx * sy, place, lane);
+            }
+        }
+        __syncthreads();
+        uint8_t *mat = a.out + a.out_offs[i];
+        const uint32_t nd = (tw + 3) / 4;
+        for (uint32_t it = tid; it < th * nd; it += 256) {
+            const uint32_t r = it / nd, d = it - r * nd;
+            uint8_t *dst = mat + (ty0 + r) * W + tx0 + 4 * d;
+            const uint32_t v = *reinterpret_cast<const uint32_t *>(T + r * kDS + 4 * d);
+            if (4 * d + 4 <= tw) {
+                typedef uint32_t u32u __attribute__((aligned(1)));
+                *reinterpret_cast<u32u *>(dst) = v;
+            } else {
+                for (uint32_t k = 0; 4 * d + k < tw; ++k) dst[k] = (uint8_t)(v >> (8 * k));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// modes 1 and 2: the blocks of one group per wave, scattered straight to memory
 __global__ __launch_bounds__(256) void unblock_kernel(DecArgs a, Ws ws)
 {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
@@ -1003,67 +1315,26 @@ __global__ __launch_bounds__(256) void unblock_kernel(DecArgs a, Ws ws)
     for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
         const uint32_t i = find_item(ws.idx[0], a.n, t);
         const AMeta &M = ws.meta[i];
-        if (M.status) continue;
+        if (M.status || M.mode == 0) continue;
         const uint64_t g = t - ws.idx[0][i];
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
-        const uint8_t *dirs = sym + 24;
-        uint64_t pos = at<uint64_t>(ws, M.starts)[g];
+        uint64_t pos = at<uint32_t>(ws, M.starts)[g];
         uint8_t *mat = a.out + a.out_offs[i];
         const uint64_t W = M.w;
         const uint64_t kb = g * M.K, ke = kb + M.K < M.nb ? kb + M.K : M.nb;
         for (uint64_t k = kb; k < ke; ++k) {
             uint64_t x0, y0, sx, sy;
             block_size(M, k, &x0, &y0, &sx, &sy);
-            const bool horiz = (dirs[k / 8] >> (7 - k % 8)) & 1;
+            const bool horiz = (sym[24 + k / 8] >> (7 - k % 8)) & 1;
             const uint64_t inner = horiz ? sx : sy, want = sx * sy;
             const bool small = want < (1u << 24);
             const float inv = 1.0f / (float)inner;
             auto place = [&](uint64_t q, uint32_t v) {
-                uint64_t a1, b1;
-                if (small) {
-                    a1 = div_small((uint32_t)q, (uint32_t)inner, inv);
-                } else {
-                    a1 = q / inner;
-                }
-                b1 = q - a1 * inner;
-                const uint64_t x = x0 + (horiz ? b1 : a1), y = y0 + (horiz ? a1 : b1);
-                mat[y * W + x] = (uint8_t)v;
+                const uint64_t a1 = small ? div_small((uint32_t)q, (uint32_t)inner, inv) : q / inner;
+                const uint64_t b1 = q - a1 * inner;
+                mat[(y0 + (horiz ? a1 : b1)) * W + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
             };
-            uint64_t got = 0;
-            uint32_t r = 0, last = 0;
-            while (got < want && pos < M.count) {  // (the bounds pass proved the block whole)
-                const uint32_t xs = sym[pos + lane];  // in range: the bounds pass proved the block whole
-                const uint32_t up = __shfl_up(xs, 1, 64);
-                const uint32_t pr = lane ? up : last;
-                const uint32_t f = xs == pr ? kFsmEq : kFsmNe;
-                uint32_t inc = f;
-                for (uint32_t off = 1; off < 64; off <<= 1) {
-                    const uint32_t gg = __shfl_up(inc, off, 64);
-                    inc = lane >= off ? fsm_then(inc, gg) : inc;
-                }
-                const uint32_t ex = __shfl_up(inc, 1, 64);
-                const uint32_t s = ((lane ? ex : kFsmId) >> (2 * r)) & 3u;
-                const uint32_t len = s == 3 ? xs : 1u;
-                const uint32_t val = s == 3 ? pr : xs;  // a count repeats the literal before it
-                uint32_t acc = len;
-                for (uint32_t off = 1; off < 64; off <<= 1) {
-                    const uint32_t gg = __shfl_up(acc, off, 64);
-                    acc += lane >= off ? gg : 0u;
-                }
-                const uint64_t need = want - got;
-                const uint64_t hit = ballot((uint64_t)acc >= need);
-                const uint32_t L = hit ? (uint32_t)__builtin_ctzll(hit) : 63u;  // last lane of this block
-                const bool mine = lane <= L;
-                const uint64_t q0 = got + acc - len;
-                uint32_t mx = mine ? len : 0u;
-                for (uint32_t d = 32; d; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-                for (uint32_t e = 0; e < mx; ++e)
-                    if (mine && e < len) place(q0 + e, val);
-                got += __shfl(acc, L, 64);
-                r = (__shfl(inc, L, 64) >> (2 * r)) & 3u;
-                last = __shfl(xs, L, 64);
-                pos += L + 1;
-            }
+            pos = revert_block(sym, pos, M.count, want, place, lane);
         }
     }
 }
@@ -1082,7 +1353,11 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(DecArgs a, Ws ws)
         const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
         const uint8_t *mat = a.out + a.out_offs[i];
         uint32_t s = 0;
-        for (uint64_t k = b + tid; k < e; k += 256) s += mat[k];
+        for (uint64_t k = b + 4 * tid; k < e; k += 1024) {  // out_offs 4-aligned, chunks 16 KB
+            uint32_t w = *reinterpret_cast<const uint32_t *>(mat + k);
+            if (k + 4 > e) w &= 0xFFFFFFFFu >> (8 * (k + 4 - e));
+            s = __builtin_amdgcn_sad_u8(w, 0u, s);
+        }
         for (uint32_t d = 32; d; d >>= 1) s += __shfl_down(s, d, 64);
         if ((tid & 63) == 0) red[tid >> 6] = s;
         __syncthreads();
@@ -1102,21 +1377,20 @@ __global__ __launch_bounds__(64) void chunk_scan_kernel(DecArgs a, Ws ws)
         for (uint64_t b = 0; b < M.chunks; b += 64) {
             const bool ok = b + lane < M.chunks;
             const uint32_t v = ok ? cs[b + lane] : 0u;
-            uint32_t acc = v;
-            for (uint32_t off = 1; off < 64; off <<= 1) {
-                const uint32_t g = __shfl_up(acc, off, 64);
-                acc += lane >= off ? g : 0u;
-            }
+            const uint32_t acc = wave_sum_incl(v);
             if (ok) cs[b + lane] = (uint8_t)(carry + acc - v);  // exclusive
-            carry += __shfl(acc, 63, 64);
+            carry += readlane(acc, 63);
         }
     }
 }
 
+// one 16 KB chunk per workgroup, 64 bytes per thread held as 16 dwords: byte prefix sums inside
+// each dword (two shifted bytewise adds), carried along the thread's dwords, then across the
+// workgroup (a scan of the threads' totals) and from the chunks before (chunk_scan_kernel)
 __global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
 {
-    __shared__ uint32_t part[256];
-    const uint32_t tid = threadIdx.x;
+    __shared__ uint32_t part[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t items = ws.ctr[1];
     for (uint64_t t = blockIdx.x; t < items; t += gridDim.x) {
         const uint32_t i = find_item(ws.idx[1], a.n, t);
@@ -1124,25 +1398,35 @@ __global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
         const uint64_t c = t - ws.idx[1][i], n = M.w * M.h;
         const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
         uint8_t *mat = a.out + a.out_offs[i];
-        // 64 bytes per thread, in order
-        const uint64_t tb = b + 64ull * tid, te = tb + 64 < e ? tb + 64 : e;
-        uint32_t s = 0;
-        for (uint64_t k = tb; k < te; ++k) s += mat[k];
-        part[tid] = s;
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t acc = at<uint8_t>(ws, M.csum)[c];
-            for (uint32_t k = 0; k < 256; ++k) {
-                const uint32_t v = part[k];
-                part[k] = acc;
-                acc += v;
-            }
+        const uint64_t tb = b + 64ull * tid;
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint64_t o = tb + 4 * k;
+            w[k] = o < e ? *reinterpret_cast<const uint32_t *>(mat + o) : 0u;
+            if (o < e && o + 4 > e) w[k] &= 0xFFFFFFFFu >> (8 * (o + 4 - e));
         }
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint32_t y = add8(w[k], w[k] << 8);
+            y = add8(y, y << 16);
+            w[k] = add8(y, run * 0x01010101u);
+            run = w[k] >> 24;
+        }
+        const uint32_t acc = wave_sum_incl(run);  // the threads' totals (mod 256)
+        if (lane == 63) part[wv] = acc;
         __syncthreads();
-        uint32_t run = part[tid];
-        for (uint64_t k = tb; k < te; ++k) {
-            run += mat[k];
-            mat[k] = (uint8_t)run;
+        uint32_t carry = at<uint8_t>(ws, M.csum)[c] + acc - run;
+        for (uint32_t k = 0; k < wv; ++k) carry += part[k];
+        carry = (carry & 0xFFu) * 0x01010101u;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint64_t o = tb + 4 * k;
+            const uint32_t v = add8(w[k], carry);
+            if (o + 4 <= e) *reinterpret_cast<uint32_t *>(mat + o) = v;
+            else
+                for (uint64_t q = o; q < e; ++q) mat[q] = (uint8_t)(v >> (8 * (q - o)));
         }
         __syncthreads();
     }
@@ -1158,6 +1442,20 @@ __global__ void dec_final_kernel(DecArgs a, Ws ws)
     else if (M.status != HC_ERR_CAPACITY) a.out_lens[i] = 0;
 }
 
+// Persistent grids: exactly the workgroups the device holds at once (CUs x resident workgroups
+// per CU at this kernel's LDS / VGPR use), so no workgroup waits for a second round.
+template <class Kernel>
+unsigned resident_grid(Kernel k, unsigned threads)
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, (int)threads, 0) != hipSuccess || cus <= 0 ||
+        per <= 0)
+        return kGrid;
+    return (unsigned)(cus * per);
+}
+
 }  // namespace
 
 uint64_t adapt_encode_work_bound(uint64_t total_in, uint32_t n)
@@ -1168,8 +1466,9 @@ uint64_t adapt_encode_work_bound(uint64_t total_in, uint32_t n)
 
 uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t n)
 {
-    // symbols <= 8 bits each of the payload; group starts <= W*H / 256 + 2; chunk sums
-    return ws_header(n) + 8 * total_in + total_out / 16 + 128ull * n + 4096;
+    // symbols <= 8 per payload byte (+64 slack); u32 block starts <= out_cap / 7 + 16 (see
+    // group_entries_bound); chunk sums out_cap / 16384
+    return ws_header(n) + 8 * total_in + total_out / 7 * 4 + total_out / kChunk + 192ull * n + 4096;
 }
 
 hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work, uint64_t work_bytes,
@@ -1179,10 +1478,11 @@ hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work
     const Ws ws = carve(work, work_bytes, b.n);
     const EncArgs a{b.in, b.in_offs, b.in_lens, widths, b.n, (b.flags & HC_FLAG_DIFF) ? 1u : 0u};
     enc_plan_kernel<<<1, 1024, 0, st>>>(a, ws);
-    tile_cost_kernel<<<kGrid, 256, 0, st>>>(a, ws);
-    big_cost_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    tile_cost_kernel<<<resident_grid(tile_cost_kernel, 256), 256, 0, st>>>(a, ws);
+    big_cost_kernel<<<resident_grid(big_cost_kernel, 256), 256, 0, st>>>(a, ws);
     choose_kernel<<<b.n < kGrid ? b.n : kGrid, 256, 0, st>>>(a, ws);
-    emit_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    emit_tile_kernel<<<resident_grid(emit_tile_kernel, 256), 256, 0, st>>>(a, ws);
+    emit_big_kernel<<<resident_grid(emit_big_kernel, 256), 256, 0, st>>>(a, ws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     Batch f = b;
@@ -1211,11 +1511,12 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
     hipError_t e = launch_decode(f, DST_SYMBOLS, st);
     if (e != hipSuccess) return e;
     dec_header_kernel<<<1, 1024, 0, st>>>(a, ws);
-    bounds_kernel<<<kGrid, 256, 0, st>>>(a, ws);
-    unblock_kernel<<<kGrid, 256, 0, st>>>(a, ws);
-    chunk_sum_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    bounds_kernel<<<resident_grid(bounds_kernel, 256), 256, 0, st>>>(a, ws);
+    unblock_tile_kernel<<<resident_grid(unblock_tile_kernel, 256), 256, 0, st>>>(a, ws);
+    unblock_kernel<<<resident_grid(unblock_kernel, 256), 256, 0, st>>>(a, ws);
+    chunk_sum_kernel<<<resident_grid(chunk_sum_kernel, 256), 256, 0, st>>>(a, ws);
     chunk_scan_kernel<<<b.n < kGrid ? b.n : kGrid, 64, 0, st>>>(a, ws);
-    undiff_kernel<<<kGrid, 256, 0, st>>>(a, ws);
+    undiff_kernel<<<resident_grid(undiff_kernel, 256), 256, 0, st>>>(a, ws);
     dec_final_kernel<<<(b.n + 255) / 256, 256, 0, st>>>(a, ws);
     return hipGetLastError();
 }

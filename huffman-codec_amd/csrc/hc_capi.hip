@@ -311,7 +311,7 @@ int hc_decompress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const 
     if (n_streams == 0) return HC_OK;
     if (!in || !in_offs || !in_lens || !out || !out_offs || !out_caps || !out_lens || !status || !work)
         return HC_ERR_ARG;
-    if (!aligned4(in) || (reinterpret_cast<uintptr_t>(work) & 15u)) return HC_ERR_ARG;
+    if (!aligned4(in) || !aligned4(out) || (reinterpret_cast<uintptr_t>(work) & 15u)) return HC_ERR_ARG;
     Batch b{in, in_offs, in_lens, n_streams, out, out_offs, out_caps, out_lens, status, 0};
     const hipError_t e = hc::adapt_decode_batch(b, work, work_bytes, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? HC_OK : HC_ERR_DEVICE;
