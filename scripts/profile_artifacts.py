@@ -2,69 +2,99 @@
 
   profiles/<round>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as written)
   profiles/<round>_pmc_summary.json   per-launch PMC counters of the FGK kernels + per-symbol rates
-  profiles/traffic.json               HBM bytes per launch for bench.py's roofline.traffic
+  profiles/pmc_summary.json           what bench.py reads for roofline.traffic and issue: per
+                                      launch HBM bytes and VALU + SALU instructions, keyed
+                                      kernel:mode:kind:streams, stamped with the sha of
+                                      hc_fgk.hip (bench.py ignores it once the source changes)
 
-    python scripts/profile_artifacts.py <tag> <round> [symbols_per_launch]
+    python scripts/profile_artifacts.py <tag> <round> [--streams S] [--mode cm] [--kind photo]
 
 HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE (KB -> B). The x2: on gfx950 FETCH_SIZE counts half of
-wide streaming reads (MI355X_MICROARCH.md, HBM / rocprofv3); our loads are 4 B/lane, which the
-guide lists as uncalibrated, so the factor is checked against a known byte count: the encoder
-must read exactly 8192 x 262144 raw bytes, and x2 FETCH_SIZE reproduces that to 0.1 %.
+wide streaming reads (MI355X_MICROARCH.md, HBM / rocprofv3); the kernels' loads are 4 B/lane,
+which the guide lists as uncalibrated, so the factor is checked against a known byte count: the
+encoder reads exactly streams x 262144 raw bytes, and x2 FETCH_SIZE reproduces that (the check
+is printed: `encoder_read_check`).
 """
+import argparse
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
+import re
 import shutil
-import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NAMES = {"encode_kernel<false, 1>": "encode_kernel<narrow,raw+diff>",
-         "decode_kernel<false, 0>": "decode_kernel<narrow,raw>"}
+FGK_SRC = os.path.join(ROOT, "huffman-codec_amd", "csrc", "hc_fgk.hip")
+
+
+def kernel_key(name):
+    """encode_kernel<false, 1> -> ('encode_kernel', narrow)"""
+    m = re.search(r"(encode_kernel|decode_kernel)<(false|true), (\d)>", name)
+    return (m.group(1), m.group(2) == "false", int(m.group(3))) if m else None
 
 
 def main():
-    tag, rnd = sys.argv[1], sys.argv[2]
-    syms = float(sys.argv[3]) if len(sys.argv) > 3 else 8192 * 201635.0
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("round")
+    ap.add_argument("--streams", type=int, default=65536)
+    ap.add_argument("--mode", default="cm")
+    ap.add_argument("--kind", default="photo")
+    ap.add_argument("--symbols", type=float, default=201635.0, help="FGK symbols per stream (photo -c -m)")
+    a = ap.parse_args()
     prof = os.path.join(ROOT, "gpurun_out", "prof")
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    shutil.copy(os.path.join(prof, f"{tag}_stats", "stats_kernel_stats.csv"),
-                os.path.join(out, f"{rnd}_kernel_stats.csv"))
+    stats = glob.glob(os.path.join(prof, f"{a.tag}_stats", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats[0], os.path.join(out, f"{a.round}_kernel_stats.csv"))
 
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     launches = collections.defaultdict(set)
-    for f in glob.glob(os.path.join(prof, f"{tag}_pmc_*", "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(prof, f"{a.tag}_pmc_*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            for k, name in NAMES.items():
-                if k in r["Kernel_Name"]:
-                    agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
-                    launches[(name, r["Counter_Name"])].add(r["Dispatch_Id"])
-    summary = {"workload": "bench.py --streams 8192 (photo -c -m, 8192 x 512x512); counters per launch",
-               "symbols_per_launch": syms,
+            k = kernel_key(r["Kernel_Name"])
+            if not k or not k[1]:  # the narrow variants code the photo streams; the wide ones exit
+                continue
+            name = k[0]
+            agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
+            launches[(name, r["Counter_Name"])].add(r["Dispatch_Id"])
+    syms = a.symbols * a.streams
+    src = hashlib.sha256(open(FGK_SRC, "rb").read()).hexdigest()[:16]
+    summary = {"workload": f"bench.py --streams {a.streams} ({a.kind} -{a.mode.replace('m', ' -m')}, 512x512); "
+                           "counters per launch", "source_sha": src, "symbols_per_launch": syms,
                "note": "rocprofv3 --pmc passes, one counter group per run (never combined with tracing); "
                        "FETCH_SIZE / WRITE_SIZE in KB as reported",
                "counters": {}, "per_symbol": {}, "hbm_bytes_per_launch": {}}
-    traffic = {}
+    bench = {"source_sha": src, "launches": {},
+             "_note": f"per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE) and SQ_INSTS_VALU + SQ_INSTS_SALU from "
+                      f"rocprofv3 PMC passes; details in profiles/{a.round}_pmc_summary.json"}
     for name, d in agg.items():
         per = {c: v / max(1, len(launches[(name, c)])) for c, v in d.items()}
         summary["counters"][name] = per
         summary["per_symbol"][name] = {c: round(per[c] / syms, 3) for c in per
                                        if c.startswith("SQ_INSTS") or c.startswith("SQ_ACTIVE") or
                                        c.startswith("SQ_WAIT") or c == "SQ_WAVE_CYCLES"}
+        e = {}
         if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
             b = int(round((per["FETCH_SIZE"] * 2 + per["WRITE_SIZE"]) * 1024))
             summary["hbm_bytes_per_launch"][name] = b
-            traffic[("encode_kernel" if "encode" in name else "decode_kernel") + ":cm:photo:8192"] = b
-    with open(os.path.join(out, f"{rnd}_pmc_summary.json"), "w") as f:
+            e["hbm_bytes"] = b
+            if name == "encode_kernel":
+                summary["encoder_read_check"] = {"fetch_x2_bytes": per["FETCH_SIZE"] * 2 * 1024,
+                                                 "raw_bytes": a.streams * 262144.0}
+        if "SQ_INSTS_VALU" in per and "SQ_INSTS_SALU" in per:
+            e["valu_salu_insts"] = per["SQ_INSTS_VALU"] + per["SQ_INSTS_SALU"]
+        bench["launches"][f"{name}:{a.mode}:{a.kind}:{a.streams}"] = e
+    with open(os.path.join(out, f"{a.round}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    traffic["_note"] = (f"HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, KB->B), "
-                        f"profiles/{rnd}_pmc_summary.json; see scripts/profile_artifacts.py for the x2 calibration")
-    with open(os.path.join(out, "traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
+    with open(os.path.join(out, "pmc_summary.json"), "w") as f:
+        json.dump(bench, f, indent=1)
     print(json.dumps(summary["per_symbol"], indent=1))
-    print(json.dumps(traffic, indent=1))
+    print(json.dumps(bench, indent=1))
+    print(json.dumps(summary.get("encoder_read_check"), indent=1))
 
 
 if __name__ == "__main__":
