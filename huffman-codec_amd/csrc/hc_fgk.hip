@@ -23,6 +23,8 @@
 //    descriptors whose hardware range check replaces per-lane bounds tests.
 //  * Output bits gather in a 64-bit scalar accumulator, flush as big-endian dwords into a VGPR
 //    stage and leave as one coalesced 256-byte buffer store per 64 words.
+#include <type_traits>
+
 #include "hc_internal.h"
 
 // llvm.amdgcn.writelane has no clang builtin in this toolchain; binding the intrinsic by name
@@ -35,6 +37,12 @@ namespace hc {
 // [3 * stream] (scripts/residency.py measures how many waves share each SIMD). Set by
 // hc_debug_set_trace (not part of include/hcodec.h); null in normal use.
 __device__ uint64_t *g_trace = nullptr;
+
+// Streams are addressed through buffer descriptors, whose offsets are 32-bit: each stream's input
+// and output are reached through windows that slide forward by whole multiples of 256 bytes
+// once the offset inside them passes g_window (1 GiB; hc_debug_set_window shrinks it so that
+// tests cross many window edges on small streams), so streams of any length fit.
+__device__ uint32_t g_window = 1u << 30;
 
 namespace {
 
@@ -801,7 +809,8 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
 // fill at most 63 words. The u64 count (words 0-1) is written at the end by the lanes that
 // stored those words first, so program order keeps it last.
 struct RecSink {
-    rsrc_t rs;
+    rsrc_t rs;           // window of the output at byte 4 * wbase
+    uint32_t wbase;      // first word of the window
     uint32_t lane;
     uint32_t *stage;  // the wave's 64 scratch words
     uint32_t vrec;    // lane k: record k of the current group
@@ -858,12 +867,21 @@ struct RecSink {
         const uint32_t word = stage[lane];
         const uint32_t total = nb + lane_read(incl, 63);
         const uint32_t full = total >> 5;  // <= 62
-        buf_store(rs, lane < full ? (wout + lane) * 4 : kDrop, __builtin_bswap32(word));
+        buf_store(rs, lane < full ? (wout - wbase + lane) * 4 : kDrop, __builtin_bswap32(word));
         pend = lane_read(word, full);
         nb = total & 31u;
         wout += full;
         n = 0;
         __builtin_amdgcn_wave_barrier();
+    }
+
+    // the window starts at the current word (stores past cap fall outside every range); called
+    // between input chunks (a chunk adds < 2 KB of output)
+    __device__ void rebase(uint8_t *out, uint64_t cap)
+    {
+        wbase = wout;
+        const uint64_t at = 4ull * wbase;
+        rs = make_rsrc(out + at, at < cap ? (uint32_t)min(cap - at, (uint64_t)kMaxBufBytes) : 0u);
     }
 
     // pack what is left, zero-pad to a byte (transform.cpp:379-381), store the last 0..4 bytes;
@@ -873,7 +891,7 @@ struct RecSink {
         if (n) pack();
         const uint32_t tail = (nb + 7u) >> 3;  // 0..4 bytes
         for (uint32_t b = 0; b < 4; ++b)
-            buf_store8(rs, lane == 0 && b < tail ? wout * 4 + b : kDrop, pend >> (24 - 8 * b));
+            buf_store8(rs, lane == 0 && b < tail ? (wout - wbase) * 4 + b : kDrop, pend >> (24 - 8 * b));
         return (uint64_t)wout * 4 + tail;
     }
 };
@@ -897,21 +915,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     const uint64_t out_off = uni64(bt.out_offs[sid]);
     const uint64_t cap = uni64(bt.out_caps[sid]);
 
-    // worst-case symbol count decides narrow / wide; the other variant's launch skips
+    // worst-case symbol count decides narrow / wide; the other variant's launch skips. The wide
+    // tree's 32-bit weights hold any stream below 2^32 - 1 symbols; the count is checked as the
+    // symbols are produced (RLE usually makes far fewer than the worst case).
     const uint64_t max_sym = kSrc == SRC_SYMBOLS ? n : n + n / 3 + 2;
     const bool narrow_ok = max_sym <= kNarrowMaxSymbols;
     if (kWide == narrow_ok) return;
-    if (max_sym > kWideMaxSymbols || n > kMaxBufBytes) {
-        if (lane == 0) {
-            bt.status[sid] = HC_ERR_UNSUPPORTED;
-            bt.out_lens[sid] = 0;
-        }
-        return;
-    }
+    const uint32_t window = uni(g_window);
 
     Fgk<kWide, false> fgk(trees[wv], lane);
     RecSink sink;
     sink.rs = make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
+    sink.wbase = 0;
     sink.lane = lane;
     sink.stage = fgk.T.scratch;
     sink.vrec = 0;
@@ -923,8 +938,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     sink.nb = 8;
     sink.wout = 2;
 
-    const uint32_t n32 = (uint32_t)n;
-    const rsrc_t rin = make_rsrc(bt.in + in_off, (n32 + 3u) & ~3u);
+    // input: 256-byte chunks ci < nch through a window; ioff = the next load's offset in it
+    rsrc_t rin = make_rsrc(bt.in + in_off, (uint32_t)min((n + 3u) & ~3ull, (uint64_t)kMaxBufBytes));
+    const uint32_t nch = (uint32_t)((n + 255) / 256);
+    uint32_t ioff = 256;
 
     // transform.cpp:363-384: per symbol encode (path before update), then update. A symbol
     // whose root path is cached (the common case) takes the hot path, written so that its
@@ -978,7 +995,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     // on the paths that leave the loop (split, insert, swap), so what was read ahead stays
     // valid inside it; the loop is re-primed after every exit. Bytes past ns are older symbols
     // of the same buffer: their reads are harmless.
-    auto code_all = [&](uint32_t ns) {
+    auto code_all = [&](uint32_t ns) __attribute__((always_inline)) {
         uint32_t t = 0;
         while (t < ns) {
             uint32_t rl = sink.n;  // record lane of symbol t (scalar)
@@ -1039,36 +1056,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     };
 
     uint64_t nsym = 0;
+    bool over = false;  // >= 2^32 - 1 symbols: beyond the wide tree's weights
     uint32_t next = buf_load(rin, lane * 4);
     RleCarry cy = {0, 0, 0};
-    for (uint32_t base = 0; base < n32 && !fgk.bad; base += 256) {
-        prio_by_progress(base, n32);
-        const uint32_t chunk = next;
-        next = buf_load(rin, base + 256 + lane * 4);  // out of range past the end: reads 0
-        const uint32_t m = min(256u, n32 - base);
-        if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
-            fgk.T.syms[lane] = chunk;
-            __builtin_amdgcn_wave_barrier();
-            code_all(m);
-            nsym += m;
-            continue;
+    // Two copies of the chunk loop: streams that fit one window (every batch stream) run without
+    // the window bookkeeping, which would otherwise sit in scalar registers across the hot loop;
+    // only the wide trees can reach 2^32 - 1 symbols.
+    auto chunks = [&](auto windowed) __attribute__((always_inline)) {
+        constexpr bool kWin = decltype(windowed)::value;
+        for (uint32_t ci = 0; ci < nch && !fgk.bad; ++ci, ioff += 256) {
+            prio_by_progress(ci, nch);
+            const uint32_t chunk = next;
+            if constexpr (kWin) {
+                if (ioff >= window) {  // slide the input window up to the next chunk
+                    const uint64_t at = 256ull * (ci + 1);
+                    rin = make_rsrc(bt.in + uni64(bt.in_offs[sid]) + at,
+                                    (uint32_t)min((n - min(n, at) + 3u) & ~3ull, (uint64_t)kMaxBufBytes));
+                    ioff = 0;
+                }
+                if ((sink.wout - sink.wbase) * 4ull >= window) sink.rebase(bt.out + out_off, cap);
+            }
+            next = buf_load(rin, ioff + lane * 4);  // out of range past the end: reads 0
+            const uint32_t m = ci + 1 < nch ? 256u : (uint32_t)(n - 256ull * ci);
+            if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
+                if (kWide && nsym + m > kWideMaxSymbols) {
+                    over = true;
+                    break;
+                }
+                fgk.T.syms[lane] = chunk;
+                __builtin_amdgcn_wave_barrier();
+                code_all(m);
+                nsym += m;
+                continue;
+            }
+            // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
+            HC_PROF_BEGIN();
+            const uint32_t ns = rle_chunk<kSrc>(chunk, m, ci + 1 == nch ? 1u : 0u, cy, fgk.T.syms,
+                                                fgk.scr32(), lane);
+            HC_PROF_END(4);
+            if (kWide && nsym + ns > kWideMaxSymbols) {
+                over = true;
+                break;
+            }
+            code_all(ns);
+            nsym += ns;
         }
-        // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
-        HC_PROF_BEGIN();
-        const uint32_t ns = rle_chunk<kSrc>(chunk, m, base + m == n32 ? 1u : 0u, cy, fgk.T.syms,
-                                            fgk.scr32(), lane);
-        HC_PROF_END(4);
-        code_all(ns);
-        nsym += ns;
-    }
+    };
+    if (n + 512 <= window && cap <= window) chunks(std::false_type{});
+    else chunks(std::true_type{});
 
     const uint64_t total = sink.finish();
-    const uint32_t st = fgk.bad ? (uint32_t)HC_ERR_DEVICE : (total <= cap ? 0u : (uint32_t)HC_ERR_CAPACITY);
+    const uint32_t st = fgk.bad ? (uint32_t)HC_ERR_DEVICE
+                                : (over ? (uint32_t)HC_ERR_UNSUPPORTED : (total <= cap ? 0u : (uint32_t)HC_ERR_CAPACITY));
     // headers.cpp:110-116: u64 little-endian symbol count in words 0-1 (stored after every
     // payload word by program order)
-    buf_store(sink.rs, lane < 2 ? lane * 4 : kDrop, lane ? (uint32_t)(nsym >> 32) : (uint32_t)nsym);
+    buf_store(make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)8)), lane < 2 ? lane * 4 : kDrop,
+              lane ? (uint32_t)(nsym >> 32) : (uint32_t)nsym);
     if (lane == 0) {
-        bt.out_lens[sid] = fgk.bad ? 0 : total;
+        bt.out_lens[sid] = (fgk.bad || over) ? 0 : total;
         bt.status[sid] = (int32_t)st;
     }
     trace_wave(sid, t0, lane);
@@ -1080,9 +1125,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
 // MSB-first reader over a stream's bytes; words come from a 64-word VGPR chunk, the next chunk
 // already loading (its wait falls ~64 refills later).
 struct BitSource {
-    rsrc_t rs;
+    rsrc_t rs;       // window of the stream at byte ibase
+    uint64_t ibase;
     uint32_t lane;
-    uint32_t cbase;  // byte offset of chunk lane 0
+    uint32_t cbase;  // byte offset of chunk lane 0 in the window
     uint32_t chunk;  // big-endian words (byte-swapped once per load, on the lanes)
     uint32_t nxt;    // the following 256 bytes as loaded
     uint32_t ridx;
@@ -1256,7 +1302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
         // decode, and the reference ends such a stream with status 9 (transform.cpp:394-398)
         if (count > (avail >= 8 ? avail - 7 : 0)) st = HC_ERR_HUFFMAN;
         else if (kDst == DST_RAW && (flags & 0x40u)) st = HC_ERR_UNSUPPORTED;
-        else if (count > kWideMaxSymbols || len > kMaxBufBytes) st = HC_ERR_UNSUPPORTED;
+        else if (count > kWideMaxSymbols) st = HC_ERR_UNSUPPORTED;
     }
     const bool narrow_ok = count <= kNarrowMaxSymbols;
     if (st == 0 && kWide == narrow_ok) return;  // the other variant's launch owns it
@@ -1271,7 +1317,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     Fgk<kWide, true> fgk(trees[wv], lane);
     BitSource in;
     in.rs = rin;
+    in.ibase = 0;
     in.lane = lane;
+    const uint32_t window = uni(g_window);
     in.cbase = 0;
     in.chunk = __builtin_bswap32(hdr);
     in.nxt = buf_load(rin, 256 + lane * 4);
@@ -1282,8 +1330,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     in.win <<= 8;
     in.nwin -= 8;
 
-    const rsrc_t rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
-    uint32_t pos = 0;  // output bytes produced
+    // output window at byte obase (slides with the output, like the input's)
+    rsrc_t rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
+    uint64_t obase = 0;
+    uint64_t pos = 0;  // output bytes produced
     const uint32_t dmask = kDst == DST_RAW && (flags & 0x80u) ? 255u : 0u;  // diff model
     RevCarry rc = {0, 0, 0};
     uint8_t *const sbuf = reinterpret_cast<uint8_t *>(fgk.T.syms);  // this block's symbols
@@ -1293,145 +1343,165 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     // range check); the reference stops there with status 9 (transform.cpp:394-398), which is
     // what the comparison after the loop reports.
     const uint64_t payload_bits = (len - 9) * 8;
-    auto consumed = [&]() -> uint64_t {
-        return (uint64_t)(in.cbase / 4 + in.ridx) * 32 - in.nwin - 72;
+    auto consumed = [&]() __attribute__((always_inline)) -> uint64_t {
+        return ((in.ibase + in.cbase) / 4 + in.ridx) * 32 - in.nwin - 72;
     };
 
-    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
-        if (fgk.bad || pos > kMaxBufBytes || consumed() > payload_bits + 64) break;
-        prio_by_progress(i0, n);
-        const uint32_t i1 = min(n, i0 + 256);
-        uint32_t i = i0;
-        while (i < i1) {
-            // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
-            // where the walk from the root stops (depth d <= 8), the levels above give the
-            // positions the walk passes.
-            if (fgk.from < 9) {
-                HC_PROF_BEGIN();
-                fgk.build_levels();
-                HC_PROF_END(5);
-            }
-            if (in.nwin <= 32) in.refill();
-            // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
-            // symbol's depth is known the next symbol's table entry is read, before this
-            // symbol's update (the tables and body[] change only on the paths that leave the
-            // loop, and the loop is re-entered after them). Anything else
-            // (a longer code or a stale table: body inner; the NYT; a failed leader test) is
-            // forced to fail at level 0 so nothing is stored, and is finished outside.
-            // lane k reads level 8 - k's entry for the code's 8-bit prefix v, at
-            // ((256 | v) >> k) - 2: levels >= d repeat the leaf's entry (position | depth d), so
-            // lanes 0..8-d hold the leaf, lanes 9-d..7 its ancestors (level 8-k), lane 8 and up
-            // the root pad (lvl_root). One read gives the depth (lane 0) and the whole root path
-            // (duplicated lanes store the same word); it depends only on the window, so the next
-            // code's read goes out as soon as this code's depth is known.
-            // ((256 | v) >> k) - 2 = (v >> k) + (256 >> k) - 2, and v >> k = window bits 56 + k..63:
-            // one per-lane shift of the window's high word and one per-lane base; lanes 8 and up
-            // shift by 31 and land on lvl_root[-2 + 0/1] (both the root)
-            const uint32_t vsh = 24 + min(lane, 7u);
-            const uint32_t vbase = lds_off16(&fgk.T.lvl[0]) + 2 * (lane < 8 ? (256u >> lane) - 2 : 0xFFFFFFFEu);
-            auto path_read = [&](uint64_t w) {
-                return opaque(*(const lds_u16 *)(size_t)(vbase + ((uint32_t)(w >> 32) >> vsh) * 2));
-            };
-            uint32_t pr = path_read(in.win);
-            const uint32_t bbase = lds_off16(&fgk.T.body[0]);
-            uint32_t d, x, b, pv, k;
-            // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
-            // both sign bits set, one scalar AND
-            int32_t left = (int32_t)(i - i1);
-            lds_u8 *so = (lds_u8 *)sbuf + (i - i0);  // the symbol's byte (LDS address in a VGPR)
-            asm("" : "+v"(so));
-            do {
-                const uint32_t e8 = uni(pr);  // the leaf's entry
-                x = e8 & 1023u;
-                d = e8 >> 10;
-                b = opaque(*(const lds_u16 *)(size_t)lshl1_add(x, bbase));
-                pv = pr & 1023u;
-                in.win <<= d;
-                in.nwin -= d;  // >= 25
-                uint32_t prn;
-                // a leaf's body is its symbol; inner / NYT (bit 15): force the failure
-                const uint32_t force = (uint32_t)__builtin_amdgcn_sbfe((int)b, 15, 1);
-                k = fgk.update_fast(pv, [&] { prn = path_read(in.win); }, force);  // the next code's
-                *so++ = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
-                ++left;
-                if (in.nwin <= 32) in.refill();
-                pr = prn;
-            } while ((int32_t)(k & (uint32_t)left) < 0);
-            i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
-            if (k == 0xFFFFFFFFu) continue;
-            // symbol i - 1 left the loop: the window stands d bits into its code
-            b = uni(b);
-            if (!(b & (kInner | kNyt))) {  // a leaf whose update reported level k: walk from there
-                HC_PROF_BEGIN();
-                fgk.walk(lane_read(pv, k), pv);
-                HC_PROF_END(1);
-                continue;
-            }
-            // nothing was stored for it
-            uint32_t sym = 0;
-            bool deep = false;  // a code longer than the cache's 9 levels: a rare symbol
-            HC_PROF_BEGIN();
-            if (b & kInner) {
-                // the code is longer than the tables reach, or they stopped short (a leaf that
-                // split since): descend bit by bit, top-down first (depth j at lane 64-j),
-                // then turned bottom-up
-                uint32_t depth = uni(d);
-                x = uni(x);
-                fgk.stale += depth < 8 ? 1u : 0u;
-                if (fgk.stale >= kRefresh) fgk.from = 0;
-                // levels 1..8 of the prefix, lane 64 - j <- level j (lane 8 - j of the path read)
-                uint32_t pt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 56) & 63u) * 4), (int)pv);
-                do {
-                    x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
-                    pt = lane == 63 - depth ? x : pt;
-                    ++depth;
-                    b = uni(fgk.T.body[x]);
-                } while ((b & kInner) && depth < 63);
-                if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
-                deep = depth > kInsertDepth;
-                pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
-                pv = lane < depth ? pv : kRoot;
-                sym = b & 255u;
-            }
-            if (b & kNyt) {  // the new leaf below the NYT becomes level 0
-                sym = in.bits8();
-                // huffman.cpp:95-111 splits only for a symbol without a leaf; a corrupted stream
-                // can name a known one, whose own leaf is then updated
-                const uint32_t known = fgk.find_leaf(sym);
-                if (known == 0xFFFFFFFFu) {
-                    x = uni(fgk.split(sym));
-                    pv = __shfl_up(pv, 1, 64);
-                    pv = lane == 0 ? x : pv;
-                } else {
-                    fgk.chase(known, pv);
+    // two copies of the block loop, as in the encoder: without window bookkeeping for streams
+    // that fit one window (input and output), with it for the rest
+    auto blocks = [&](auto windowed) __attribute__((always_inline)) {
+        constexpr bool kWin = decltype(windowed)::value;
+        for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+            if (fgk.bad || consumed() > payload_bits + 64) break;
+            if constexpr (kWin) {
+                if (in.cbase >= window) {  // slide the input window to the current chunk (a block of
+                    in.ibase += in.cbase;  // 256 symbols reads < 2 KB, so offsets stay below 2^31)
+                    in.cbase = 0;
+                    const uint64_t l = uni64(bt.in_lens[sid]);
+                    in.rs = make_rsrc(bt.in + uni64(bt.in_offs[sid]) + in.ibase,
+                                      (uint32_t)min((l - min(l, in.ibase) + 3u) & ~3ull, (uint64_t)kMaxBufBytes));
+                }
+                if (pos - obase >= window) {  // and the output window to the next byte
+                    obase = pos;
+                    rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]) + obase,
+                                     obase < cap ? (uint32_t)min(cap - obase, (uint64_t)kMaxBufBytes) : 0u);
                 }
             }
-            HC_PROF_END(2);
-            if (!(b & kInner)) {
+            prio_by_progress(i0, n);
+            const uint32_t i1 = min(n, i0 + 256);
+            uint32_t i = i0;
+            while (i < i1) {
+                // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
+                // where the walk from the root stops (depth d <= 8), the levels above give the
+                // positions the walk passes.
+                if (fgk.from < 9) {
+                    HC_PROF_BEGIN();
+                    fgk.build_levels();
+                    HC_PROF_END(5);
+                }
+                if (in.nwin <= 32) in.refill();
+                // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
+                // symbol's depth is known the next symbol's table entry is read, before this
+                // symbol's update (the tables and body[] change only on the paths that leave the
+                // loop, and the loop is re-entered after them). Anything else
+                // (a longer code or a stale table: body inner; the NYT; a failed leader test) is
+                // forced to fail at level 0 so nothing is stored, and is finished outside.
+                // lane k reads level 8 - k's entry for the code's 8-bit prefix v, at
+                // ((256 | v) >> k) - 2: levels >= d repeat the leaf's entry (position | depth d), so
+                // lanes 0..8-d hold the leaf, lanes 9-d..7 its ancestors (level 8-k), lane 8 and up
+                // the root pad (lvl_root). One read gives the depth (lane 0) and the whole root path
+                // (duplicated lanes store the same word); it depends only on the window, so the next
+                // code's read goes out as soon as this code's depth is known.
+                // ((256 | v) >> k) - 2 = (v >> k) + (256 >> k) - 2, and v >> k = window bits 56 + k..63:
+                // one per-lane shift of the window's high word and one per-lane base; lanes 8 and up
+                // shift by 31 and land on lvl_root[-2 + 0/1] (both the root)
+                const uint32_t vsh = 24 + min(lane, 7u);
+                const uint32_t vbase = lds_off16(&fgk.T.lvl[0]) + 2 * (lane < 8 ? (256u >> lane) - 2 : 0xFFFFFFFEu);
+                auto path_read = [&](uint64_t w) __attribute__((always_inline)) {
+                    return opaque(*(const lds_u16 *)(size_t)(vbase + ((uint32_t)(w >> 32) >> vsh) * 2));
+                };
+                uint32_t pr = path_read(in.win);
+                const uint32_t bbase = lds_off16(&fgk.T.body[0]);
+                uint32_t d, x, b, pv, k;
+                // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
+                // both sign bits set, one scalar AND
+                int32_t left = (int32_t)(i - i1);
+                lds_u8 *so = (lds_u8 *)sbuf + (i - i0);  // the symbol's byte (LDS address in a VGPR)
+                asm("" : "+v"(so));
+                do {
+                    const uint32_t e8 = uni(pr);  // the leaf's entry
+                    x = e8 & 1023u;
+                    d = e8 >> 10;
+                    b = opaque(*(const lds_u16 *)(size_t)lshl1_add(x, bbase));
+                    pv = pr & 1023u;
+                    in.win <<= d;
+                    in.nwin -= d;  // >= 25
+                    uint32_t prn;
+                    // a leaf's body is its symbol; inner / NYT (bit 15): force the failure
+                    const uint32_t force = (uint32_t)__builtin_amdgcn_sbfe((int)b, 15, 1);
+                    k = fgk.update_fast(pv, [&] { prn = path_read(in.win); }, force);  // the next code's
+                    *so++ = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
+                    ++left;
+                    if (in.nwin <= 32) in.refill();
+                    pr = prn;
+                } while ((int32_t)(k & (uint32_t)left) < 0);
+                i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
+                if (k == 0xFFFFFFFFu) continue;
+                // symbol i - 1 left the loop: the window stands d bits into its code
+                b = uni(b);
+                if (!(b & (kInner | kNyt))) {  // a leaf whose update reported level k: walk from there
+                    HC_PROF_BEGIN();
+                    fgk.walk(lane_read(pv, k), pv);
+                    HC_PROF_END(1);
+                    continue;
+                }
+                // nothing was stored for it
+                uint32_t sym = 0;
+                bool deep = false;  // a code longer than the cache's 9 levels: a rare symbol
                 HC_PROF_BEGIN();
-                // a rare symbol's leaf nearly always ties with the next position (9 in 10 on
-                // the slot-form model): walk from the leaf at once
-                if (deep) fgk.walk(lane_read(pv, 0), pv);
-                else fgk.update_path(pv);
-                HC_PROF_END(3);
+                if (b & kInner) {
+                    // the code is longer than the tables reach, or they stopped short (a leaf that
+                    // split since): descend bit by bit, top-down first (depth j at lane 64-j),
+                    // then turned bottom-up
+                    uint32_t depth = uni(d);
+                    x = uni(x);
+                    fgk.stale += depth < 8 ? 1u : 0u;
+                    if (fgk.stale >= kRefresh) fgk.from = 0;
+                    // levels 1..8 of the prefix, lane 64 - j <- level j (lane 8 - j of the path read)
+                    uint32_t pt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 56) & 63u) * 4), (int)pv);
+                    do {
+                        x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
+                        pt = lane == 63 - depth ? x : pt;
+                        ++depth;
+                        b = uni(fgk.T.body[x]);
+                    } while ((b & kInner) && depth < 63);
+                    if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
+                    deep = depth > kInsertDepth;
+                    pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
+                    pv = lane < depth ? pv : kRoot;
+                    sym = b & 255u;
+                }
+                if (b & kNyt) {  // the new leaf below the NYT becomes level 0
+                    sym = in.bits8();
+                    // huffman.cpp:95-111 splits only for a symbol without a leaf; a corrupted stream
+                    // can name a known one, whose own leaf is then updated
+                    const uint32_t known = fgk.find_leaf(sym);
+                    if (known == 0xFFFFFFFFu) {
+                        x = uni(fgk.split(sym));
+                        pv = __shfl_up(pv, 1, 64);
+                        pv = lane == 0 ? x : pv;
+                    } else {
+                        fgk.chase(known, pv);
+                    }
+                }
+                HC_PROF_END(2);
+                if (!(b & kInner)) {
+                    HC_PROF_BEGIN();
+                    // a rare symbol's leaf nearly always ties with the next position (9 in 10 on
+                    // the slot-form model): walk from the leaf at once
+                    if (deep) fgk.walk(lane_read(pv, 0), pv);
+                    else fgk.update_path(pv);
+                    HC_PROF_END(3);
+                }
+                sbuf[i - 1 - i0] = (uint8_t)sym;
             }
-            sbuf[i - 1 - i0] = (uint8_t)sym;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t x4 = fgk.T.syms[lane];
+            const uint32_t m = i1 - i0;
+            if (kDst == DST_SYMBOLS) {
+                for (uint32_t b = 0; b < 4; ++b)
+                    buf_store8(rout, lane * 4 + b < m ? (uint32_t)(pos - obase) + lane * 4 + b : kDrop, byte_of(x4, b));
+                pos += m;
+            } else {
+                HC_PROF_BEGIN();
+                pos += revert_block(x4, m, rc, dmask, rout, (uint32_t)(pos - obase), lane);
+                HC_PROF_END(4);
+            }
         }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t x4 = fgk.T.syms[lane];
-        const uint32_t m = i1 - i0;
-        if (kDst == DST_SYMBOLS) {
-            for (uint32_t b = 0; b < 4; ++b)
-                buf_store8(rout, lane * 4 + b < m ? pos + lane * 4 + b : kDrop, byte_of(x4, b));
-            pos += m;
-        } else {
-            HC_PROF_BEGIN();
-            pos += revert_block(x4, m, rc, dmask, rout, pos, lane);
-            HC_PROF_END(4);
-        }
-    }
+    };
+    if (len + 512 <= window && cap <= window) blocks(std::false_type{});
+    else blocks(std::true_type{});
     if (consumed() > payload_bits) st = HC_ERR_HUFFMAN;  // ran past the payload
-    else if (pos > kMaxBufBytes) st = HC_ERR_UNSUPPORTED;  // beyond the device path's offsets
     if (fgk.bad) st = HC_ERR_DEVICE;
     if (st == 0 && pos > cap) st = HC_ERR_CAPACITY;
     if (lane == 0) {
@@ -1480,6 +1550,14 @@ hipError_t launch_decode(const Batch &b, DecDst dst, hipStream_t st)
 }
 
 }  // namespace hc
+
+extern "C" int hc_debug_set_window(uint32_t bytes)
+{
+    // a multiple of 256 in [4096, 2^30]: the descriptor windows of every later FGK launch
+    uint32_t w = bytes < 4096u ? 4096u : (bytes > (1u << 30) ? (1u << 30) : bytes);
+    w &= ~255u;
+    return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_window), &w, sizeof(w)) == hipSuccess ? 0 : HC_ERR_DEVICE;
+}
 
 extern "C" int hc_debug_set_trace(void *dev_buf)
 {

@@ -279,6 +279,17 @@ def synth_batch(kind, k0, n_streams, width, height, out, stride, stream=None):
         raise HCodecError(f"hc_synth_batch failed: {rc}")
 
 
+def debug_set_window(nbytes):
+    """Test hook (not part of include/hcodec.h): the FGK kernels reach each stream through buffer
+    windows that slide every `nbytes` (default 1 GiB); a small window makes ordinary streams
+    cross many window edges. Affects every later launch in this process."""
+    f = lib().hc_debug_set_window
+    f.argtypes = [ctypes.c_uint32]
+    rc = f(int(nbytes))
+    if rc:
+        raise HCodecError(f"hc_debug_set_window failed: {rc}")
+
+
 def compress_bound(n, use_adapt=False):
     return int(lib().hc_compress_bound(n, int(bool(use_adapt))))
 

@@ -18,7 +18,7 @@ step() {  # step <log> <seconds> <cmd...>: run one GPU step, stop the script on 
     return $rc
 }
 rm -f gpurun_out/gpu_tests.log gpurun_out/bench.log
-step gpu_tests.log 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --durations=15 -k "not 4096"
-step gpu_tests.log 600 python -u -m pytest tests -m gpu -v -rf --timeout 500 -k "4096"
+step gpu_tests.log 1000 python -u -m pytest tests -m gpu -v -rf --timeout 600 --timeout-method thread --durations=15 -k "not 4096"
+step gpu_tests.log 600 python -u -m pytest tests -m gpu -v -rf --timeout 500 --timeout-method thread -k "4096"
 step bench.log 600 python -u bench.py "$@"
 tail -3 gpurun_out/bench.log
