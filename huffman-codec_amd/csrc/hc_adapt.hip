@@ -29,7 +29,8 @@
 // Decode:
 //   plan / FGK decode to symbols / parse headers (10, 11, 66, 67, capacity) / scan groups;
 //   bounds    one wave per stream: where every K-th block starts (a wave scan of the revert
-//             machine's transition functions and output lengths per 256 symbols), reporting
+//             machine's transition functions and output lengths per 512 symbols, the next step's
+//             dword loads in flight), reporting
 //             13 / 14 / 15 where the reference exits;
 //   unblock   one wave per group of K blocks (>= 1024 bytes): revert + scatter in scan order;
 //   undiff    per 16 KB chunk: byte sums, a per-stream scan of them, byte prefix sums.
@@ -1098,11 +1099,17 @@ __device__ __forceinline__ uint32_t block_size(const AMeta &m, uint64_t k, uint6
 
 // Where the blocks start (transform.cpp:330-361 running revertRLEBlock, transform.cpp:162-187,
 // block by block), reporting 13 / 14 / 15 exactly where the reference exits. One wave per
-// stream, 256 symbols per step (4 per lane); a scan of the transition functions gives each
-// symbol's state, hence its output length (count: the symbol, literal: 1); a scan of lengths
-// finds the first symbol where the block's byte count is reached. A block that ends inside the
-// step re-scans the rest of the same registers from state 0. The start of every K-th block is
-// recorded for the unblock waves.
+// stream, 512 symbols per step (8 per lane, from dword loads re-aligned by v_alignbyte, the next
+// step's already in flight: a step always advances by 512 until the last block closes); a scan
+// of the transition functions gives each symbol's state, hence its output length (count: the
+// symbol, literal: 1); a scan of lengths finds the first symbol where the block's byte count is
+// reached. A block that ends inside the step re-scans the rest of the same registers from state
+// 0. The start of every K-th block is recorded for the unblock waves.
+#ifndef HC_BOUNDS_W
+#define HC_BOUNDS_W 2
+#endif
+constexpr uint32_t kBW = HC_BOUNDS_W;   // symbol dwords per lane and step
+constexpr uint32_t kBStep = 256 * kBW;  // symbols per step
 __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
 {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
@@ -1121,6 +1128,14 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
             return k % M.K ? ~0ull : k / M.K;
         };
         const uint64_t nsym = M.count, nb = M.nb;
+        // the dwords behind symbols p + kBStep * ... of lane `lane` (the slab is 16-aligned and
+        // holds 64 bytes of slack past the symbols; dwords starting past them read as 0)
+        const uint32_t *sw = reinterpret_cast<const uint32_t *>(sym);
+        auto load = [&](uint64_t p, uint32_t *w) {
+            const uint64_t d = (p >> 2) + kBW * lane;
+#pragma unroll
+            for (uint32_t j = 0; j <= kBW; ++j) w[j] = 4 * (d + j) < nsym ? sw[d + j] : 0u;
+        };
         uint64_t pos = M.hdr;
         uint64_t blk = 0, got = 0;
         uint32_t r = 0, last = 0;
@@ -1132,34 +1147,43 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
             block_size(M, 0, &x0, &y0, &sx, &sy);
             want = sx * sy;
         }
+        uint32_t cur[kBW + 1];
+        load(pos, cur);
         while (blk < nb) {
             const uint64_t avail = nsym - pos;
-            const uint32_t m = avail < 256 ? (uint32_t)avail : 256u;
+            const uint32_t m = avail < kBStep ? (uint32_t)avail : kBStep;
             if (m == 0) {  // transform.cpp:170-174: the block wants more, the stream is empty
                 status = HC_ERR_BLOCK_EOF;
                 break;
             }
-            uint32_t x[4];
+            uint32_t nxt[kBW + 1];
+            load(pos + kBStep, nxt);  // the next step's symbols, in flight during this one
+            constexpr uint32_t kB = 4 * kBW;
+            uint32_t x[kB];
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) x[k] = 4 * lane + k < m ? sym[pos + 4 * lane + k] : 0u;
-            const uint32_t up = lane_shr1(x[3], last);
+            for (uint32_t j = 0; j < kBW; ++j) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(cur[j + 1], cur[j], (uint32_t)(pos & 3));
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) x[4 * j + k] = kB * lane + 4 * j + k < m ? (w >> (8 * k)) & 255u : 0u;
+            }
+            const uint32_t up = lane_shr1(x[kB - 1], last);
             uint32_t lo = 0;  // symbols below lo belong to blocks already closed
             bool stop = false;
             for (;;) {
-                uint32_t f[4], F = kFsmId;
+                uint32_t f[kB], F = kFsmId;
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
-                    const uint32_t ii = 4 * lane + k;
+                for (uint32_t k = 0; k < kB; ++k) {
+                    const uint32_t ii = kB * lane + k;
                     const uint32_t p = k ? x[k - 1] : up;
                     f[k] = (ii >= lo && ii < m) ? (x[k] == p ? kFsmEq : kFsmNe) : kFsmId;
                     F = fsm_then(f[k], F);
                 }
                 const uint32_t inc = fsm_scan(F);
                 uint32_t s = fsm_at(lane_shr1(inc, kFsmId), r);
-                uint32_t len[4], tot = 0;
+                uint32_t len[kB], tot = 0;
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
-                    const uint32_t ii = 4 * lane + k;
+                for (uint32_t k = 0; k < kB; ++k) {
+                    const uint32_t ii = kB * lane + k;
                     len[k] = (ii >= lo && ii < m) ? (s == 3 ? x[k] : 1u) : 0u;
                     tot += len[k];
                     s = fsm_at(f[k], s);
@@ -1170,17 +1194,20 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
                 if (!hit) {  // the block goes on past this step
                     got += readlane(acc, 63);
                     r = fsm_at(readlane(inc, 63), r);
-                    last = readlane(x[(m - 1) & 3u], (m - 1) >> 2);
+                    uint32_t lx = x[0];
+#pragma unroll
+                    for (uint32_t k = 1; k < kB; ++k) lx = ((m - 1) % kB) == k ? x[k] : lx;
+                    last = readlane(lx, (m - 1) / kB);
                     pos += m;
                     break;
                 }
                 const uint32_t L = (uint32_t)__builtin_ctzll(hit);
                 uint32_t c = acc - tot, j = 0xFFFFFFFFu, cj = 0;
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
+                for (uint32_t k = 0; k < kB; ++k) {
                     c += len[k];
                     if (j == 0xFFFFFFFFu && (uint64_t)c >= need) {
-                        j = 4 * lane + k;
+                        j = kB * lane + k;
                         cj = c;
                     }
                 }
@@ -1212,6 +1239,8 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
                 }
             }
             if (stop) break;
+#pragma unroll
+            for (uint32_t j = 0; j <= kBW; ++j) cur[j] = nxt[j];
         }
         if (status == 0 && pos != nsym) status = HC_ERR_LEFTOVER;  // transform.cpp:354-358
         if (lane == 0) M.status = status;

@@ -44,6 +44,18 @@ __device__ uint64_t *g_trace = nullptr;
 // tests cross many window edges on small streams), so streams of any length fit.
 __device__ uint32_t g_window = 1u << 30;
 
+// Diagnostic: the lowest tree layout (0 narrow, 1 wide, 2 huge) any stream may use; set by
+// hc_debug_set_min_tree so that tests run the wide and huge kernels on small streams. The
+// launchers pass it in Batch::min_tree.
+static uint32_t g_min_tree = 0;
+
+// the tree layout for a stream of at most `max_sym` FGK symbols
+__device__ __forceinline__ uint32_t tree_kind(uint64_t max_sym, uint32_t lo)
+{
+    const uint32_t k = max_sym <= kNarrowMaxSymbols ? 0u : (max_sym <= kWideMaxSymbols ? 1u : 2u);
+    return k > lo ? k : lo;
+}
+
 namespace {
 
 __device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t lane)
@@ -86,7 +98,8 @@ __device__ __forceinline__ void prof_store(uint32_t sid, uint64_t t0, uint64_t p
 // SIMD's 8 waves run ahead and the last ones finish long after, on a half-empty SIMD. Waves
 // that are behind (by the share of their stream done: below 1/2, 4/5, 19/20, the rest) take a
 // higher priority instead. Within a band the arbiter goes by age, so the last bands are short.
-__device__ __forceinline__ void prio_by_progress(uint32_t done, uint32_t total)
+template <class I>  // uint32_t, or uint64_t for the huge layout's symbol counts
+__device__ __forceinline__ void prio_by_progress(I done, I total)
 {
     const uint64_t d = (uint64_t)done * 20;
     if (d < 10ull * total) __builtin_amdgcn_s_setprio(3);
@@ -99,7 +112,10 @@ constexpr uint32_t kRoot = 512;
 constexpr uint32_t kWords = 576;  // positions 0..512 + sentinels 513..575 (s + 63)
 constexpr uint32_t kInner = 0x100;
 constexpr uint32_t kNyt = 0x200;
-constexpr int kWaves = 4;
+#ifndef HC_WAVES
+#define HC_WAVES 4
+#endif
+constexpr int kWaves = HC_WAVES;  // wavefronts (streams) per workgroup
 constexpr uint32_t kMaxBufBytes = 0x7FFFFF00u;  // per-stream limit of the 32-bit buffer offsets
 constexpr uint32_t kDrop = 0x7FFFFFF8u;         // buffer offset past every range: access dropped
 
@@ -130,18 +146,24 @@ constexpr uint32_t kMarkShift = 10; // decoder: body bits 10..14 = table generat
 constexpr uint32_t kNotLeaf = 0x8000; // decoder: body bit 15 = inner or NYT (moves with the content)
 constexpr uint32_t kContent = 0x83FF; // decoder: the body bits that move with the content
 
-// One wavefront's LDS; <= 5 KB so that 8 four-wave workgroups fit a CU. Encoder and decoder
-// each add their cache (tests/fgk_cache_model.py is the executable model of both, checked
-// against the plain slot form).
-template <bool kWide, bool kDec>
+// Tree layouts by the stream's FGK symbol count (the root's weight): kW = 0 "narrow" (<= 2^22 - 2
+// symbols: weight << 10 | parent in one u32), 1 "wide" (< 2^32 - 1: u32 weight, u16 parent), 2
+// "huge" (any count: u64 weight, as the reference's uint64_t freq, huffman.hpp:26).
+template <int kW>
+using WeightT = std::conditional_t<kW == 2, uint64_t, uint32_t>;
+
+// One wavefront's LDS; <= 5 KB so that 8 four-wave workgroups fit a CU (narrow). Encoder and
+// decoder each add their cache (tests/fgk_cache_model.py is the executable model of both,
+// checked against the plain slot form).
+template <int kW, bool kDec>
 struct alignas(16) Tree {
-    uint32_t wt[kWords];              // narrow: weight << 10 | parent; wide: weight
-    uint32_t scratch[64];             // landing words of lanes that must not write
+    WeightT<kW> wt[kWords];           // narrow: weight << 10 | parent; wide / huge: weight
+    uint32_t scratch[kW == 2 ? 128 : 64];  // landing words of lanes that must not write
     // symbol | kInner + child pair | kNyt; decoder: bits 10..15 = generation of the level
     // tables that walked through this position
     uint16_t body[516];
     uint16_t where[kDec ? 2 : 256];   // encoder: symbol -> position | (entry + 1) << 10; 0 = unseen
-    uint16_t up[kWide ? 516 : 2];     // wide: parent position
+    uint16_t up[kW ? 516 : 2];        // wide / huge: parent position
     // encoder path cache, entry e = row e: positions of levels 0..11 (kRoot above the path),
     // [12] code record 1 << depth | code bits, [13] depth | valid << 5 | symbol << 8, [14..15]
     // unused. One lane-based
@@ -163,7 +185,11 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;  // a byte in LDS (32-
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 // the 32-bit LDS address of a word of the wave's tree
-__device__ __forceinline__ uint32_t lds_off(uint32_t *p) { return (uint32_t)(size_t)(lds_u32 *)p; }
+template <class P>
+__device__ __forceinline__ uint32_t lds_off(P *p)
+{
+    return (uint32_t)(size_t)(__attribute__((address_space(3))) P *)p;
+}
 __device__ __forceinline__ uint32_t lds_off16(uint16_t *p) { return (uint32_t)(size_t)(lds_u16 *)p; }
 // b + 2 a on the scalar unit, one instruction (wave-uniform operands)
 __device__ __forceinline__ uint32_t lshl1_add(uint32_t a, uint32_t b)
@@ -250,11 +276,14 @@ __device__ __forceinline__ void buf_store8(rsrc_t r, uint32_t off, uint32_t v)
 
 // ------------------------------------------------------------------------------ the tree --
 
-template <bool kWide, bool kDec>
+template <int kW, bool kDec>
 struct Fgk {
-    static constexpr uint32_t kInc = kWide ? 1u : 1024u;
+    static constexpr bool kWide = kW != 0;  // weights apart from parents (wide / huge)
+    static constexpr bool kHuge = kW == 2;  // 64-bit weights
+    using Wt = WeightT<kW>;
+    static constexpr Wt kInc = kWide ? 1u : 1024u;
 
-    Tree<kWide, kDec> &T;
+    Tree<kW, kDec> &T;
     uint32_t lane;
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
@@ -269,7 +298,7 @@ struct Fgk {
     const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
     uint64_t pacc = 0;        // HC_PROF regions inside the tree code
 
-    __device__ Fgk(Tree<kWide, kDec> &t, uint32_t l)
+    __device__ Fgk(Tree<kW, kDec> &t, uint32_t l)
         : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), pc_lb(0), pc_lb_ok(0), gen(0), stale(0), from(0),
           pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
     {
@@ -277,7 +306,7 @@ struct Fgk {
         // narrow: sentinels above every weight word; the encoder's last word (above kMissPos)
         // is 0 and the decoder's are all ones - 1, see update_fast
         for (uint32_t i = lane; i < kWords; i += 64)
-            T.wt[i] = i <= kRoot ? 0u : (kWide ? 0xFFFFFFFFu : (kDec ? 0xFFFFFFFEu : (i != kWords - 1 ? 0xFFFFFFFFu : 0u)));
+            T.wt[i] = i <= kRoot ? (Wt)0 : (kWide ? ~(Wt)0 : (Wt)(kDec ? 0xFFFFFFFEu : (i != kWords - 1 ? 0xFFFFFFFFu : 0u)));
         if (lane < 2) T.lvl_root[lane] = kRoot;
         for (uint32_t i = lane; i < 516; i += 64) {
             T.body[i] = i == kRoot ? (kDec ? kNyt | kNotLeaf : kNyt) : 0;
@@ -298,6 +327,19 @@ struct Fgk {
         return reinterpret_cast<uint16_t *>(&T.scratch[lane]);
     }
     __device__ __forceinline__ uint8_t *scr8() const { return reinterpret_cast<uint8_t *>(&T.scratch[lane]); }
+    // ... and a weight-sized one
+    __device__ __forceinline__ Wt *scrw() const { return reinterpret_cast<Wt *>(&T.scratch[kHuge ? 2 * lane : lane]); }
+    // a weight read on the lanes, made wave-uniform / taken from lane l
+    static __device__ __forceinline__ Wt uniw(Wt x)
+    {
+        if constexpr (kHuge) return uni64(x);
+        else return uni(x);
+    }
+    static __device__ __forceinline__ Wt readw(Wt x, uint32_t l)
+    {
+        if constexpr (kHuge) return (uint64_t)lane_read((uint32_t)x, l) | ((uint64_t)lane_read((uint32_t)(x >> 32), l) << 32);
+        else return lane_read(x, l);
+    }
 
     // ---- encoder path cache: root paths of recently coded symbols (tests/fgk_cache_model.py).
     // A path changes only when a swap moves a position on it; splits touch no symbol's path.
@@ -351,8 +393,12 @@ struct Fgk {
     {
         if (pc_lb_ok) return;
         pc_lb_ok = 1;
+        if constexpr (kHuge) {  // no bound: every swap scans the cache
+            pc_lb = 0;
+            return;
+        }
         const uint32_t p0 = T.pc[(lane & (kSlots - 1)) * kRow];  // row (lane & 15)'s leaf
-        const uint32_t w0 = T.wt[min(p0, kRoot)];
+        const uint32_t w0 = (uint32_t)T.wt[min(p0, kRoot)];
         uint32_t lw = p0 <= kRoot ? (kWide ? w0 : w0 >> 10) : 0xFFFFFFFFu;  // 0xFFFF: unused row
         lw = min(lw, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)lw, 0x111, 0xF, 0xF, false));
         lw = min(lw, (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)lw, 0x112, 0xF, 0xF, false));
@@ -451,7 +497,7 @@ struct Fgk {
         const uint32_t bval = lane == 0 ? (kInner | nl | ((t - 2) >> 1)) : (lane == 1 ? kNyt | nl : sym);
         *(lane < 3 ? &T.body[bpos] : scr16()) = (uint16_t)bval;
         if (!kDec) *(lane == 0 ? &T.where[sym] : scr16()) = (uint16_t)(t - 1);
-        if (kWide) *(lane < 2 ? &T.up[t - 2 + lane] : scr16()) = (uint16_t)t;
+        if constexpr (kWide) *(lane < 2 ? &T.up[t - 2 + lane] : scr16()) = (uint16_t)t;
         else *(lane < 2 ? &T.wt[t - 2 + lane] : scr32()) = t;  // weight 0, parent t
         __builtin_amdgcn_wave_barrier();
         nyt = t - 2;
@@ -486,7 +532,7 @@ struct Fgk {
         }
         const bool inner = lane < 4 && (b & kInner);
         const uint32_t c = (b & 255u) * 2 + (lane >> 1);
-        if (kWide) {
+        if constexpr (kWide) {
             *(inner ? &T.up[c] : scr16()) = (uint16_t)pos;
         } else {
             uint32_t *q = inner ? &T.wt[c] : scr32();
@@ -497,9 +543,9 @@ struct Fgk {
 
     // highest position >= from whose weight equals that of word w, when positions
     // from-64..from-1 all had it (the sentinels above the root end the scan)
-    __device__ uint32_t leader_far(uint32_t from, uint32_t w)
+    __device__ uint32_t leader_far(uint32_t from, Wt w)
     {
-        const uint32_t lim = kWide ? w : (w | 1023u);
+        const Wt lim = kWide ? w : (w | 1023u);
         for (;;) {
             const uint64_t le = ballot(T.wt[min(from + lane, kWords - 1)] <= lim);
             if (le != ~0ull) return from + (uint32_t)__builtin_ctzll(~le) - 1;
@@ -523,7 +569,7 @@ struct Fgk {
 
     __device__ __forceinline__ uint32_t parent(uint32_t x) const
     {
-        return kWide ? uni(T.up[x]) : (uni(T.wt[x]) & 1023u);
+        return kWide ? uni(T.up[x]) : (uni((uint32_t)T.wt[x]) & 1023u);
     }
 
     // Encoder: the path from position s to the root, BEFORE the update (the code of
@@ -543,7 +589,7 @@ struct Fgk {
                 const uint32_t sh = __builtin_amdgcn_update_dpp(0u, td, 0x138, 0xF, 0xF, true);
                 td = lane == 0 ? s : sh;
                 ++km;
-                s = kWide ? (uint32_t)T.up[s] : (T.wt[s] & 1023u);
+                s = kWide ? (uint32_t)T.up[s] : ((uint32_t)T.wt[s] & 1023u);
                 if (uni(s) == kRoot) break;
             }
             const uint32_t c = uni(s);
@@ -579,7 +625,7 @@ struct Fgk {
             const uint32_t sh = __builtin_amdgcn_update_dpp(0u, td, 0x138, 0xF, 0xF, true);
             td = lane == 0 ? s : sh;
             ++km;
-            s = kWide ? (uint32_t)T.up[s] : (T.wt[s] & 1023u);
+            s = kWide ? (uint32_t)T.up[s] : ((uint32_t)T.wt[s] & 1023u);
             // go on while s is not the root (x - 1 >= 0) and fewer than 64 levels (km < 0;
             // parents sit above children, so this only bounds a bug): one sign test
         } while ((int32_t)((uint32_t)km & ~((uni(s) ^ kRoot) - 1u)) < 0);
@@ -607,13 +653,13 @@ struct Fgk {
     __device__ void walk(uint32_t s, uint32_t pv, bool bounded = false)
     {
         for (;;) {
-            const uint32_t v = T.wt[s + lane];  // sentinels cover s + 63 <= 575
-            uint32_t ws = uni(v);
+            const Wt v = T.wt[s + lane];  // sentinels cover s + 63 <= 575
+            Wt ws = uniw(v);
             const uint64_t le = ballot(v <= (kWide ? ws : (ws | 1023u)));
-            uint32_t p = kWide ? uni(T.up[s]) : (ws & 1023u);
+            uint32_t p = kWide ? uni(T.up[s]) : ((uint32_t)ws & 1023u);
             // lane 0 read position s: its address and word, incremented, are the store's
-            uint32_t *dst = &T.wt[s + lane];
-            uint32_t nv = v + kInc;
+            Wt *dst = &T.wt[s + lane];
+            Wt nv = v + kInc;
             if ((uint32_t)le & 2u) {  // s+1 weighs the same: find the block leader
                 const uint32_t lead =
                     ~le ? s + (uint32_t)__builtin_ctzll(~le) - 1 : leader_far(s + 64, ws);
@@ -622,14 +668,14 @@ struct Fgk {
                     // the swap rewrites only parent fields below s and lead, never their own
                     // words, so the pre-swap read still holds lead's word when in range
                     const uint32_t off = lead - s;
-                    ws = off < 64 ? lane_read(v, off) : uni(T.wt[lead]);
+                    ws = off < 64 ? readw(v, off) : uniw(T.wt[lead]);
                     s = lead;
-                    p = kWide ? uni(T.up[s]) : (ws & 1023u);
+                    p = kWide ? uni(T.up[s]) : ((uint32_t)ws & 1023u);
                     dst = &T.wt[s];
                     nv = ws + kInc;
                 }
             }
-            *(lane == 0 ? dst : scr32()) = nv;
+            *(lane == 0 ? dst : scrw()) = nv;
             __builtin_amdgcn_wave_barrier();
             // chase from the parent until a position of pv; lane j of td: the j-th one passed
             uint32_t c = p, n = 0, td = kRoot;
@@ -640,7 +686,7 @@ struct Fgk {
                     bad = 1;
                     return;
                 }
-                c = kWide ? uni(T.up[c]) : (uni(T.wt[c]) & 1023u);
+                c = kWide ? uni(T.up[c]) : (uni((uint32_t)T.wt[c]) & 1023u);
             }
             // lane j < n: chased; lane j >= n: pv's lane j - n + m (kRoot past its lane 63)
             const uint32_t src = lane - n + ff1(on);
@@ -667,9 +713,10 @@ struct Fgk {
     template <class Ahead>
     __device__ __forceinline__ uint32_t update_fast(uint32_t a, Ahead &&ahead, uint32_t force = 0)
     {
-        const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
+        const Wt w0 = T.wt[a], w1 = T.wt[a + 1];
         ahead();  // the caller's reads for later symbols go out behind these
-        const uint32_t nv = w0 + kInc;
+        const Wt nv = w0 + kInc;
+        const Wt fw = (Wt)0 - (Wt)(force & 1u);  // force as a weight-wide mask
         // narrow: w1 < w0 + 1024 (the increment stored anyway) reports every level whose next
         // position is not heavier, and falsely (the walk then decides) only one whose next
         // position is exactly one heavier with a lower parent field (parents grow with the
@@ -677,12 +724,12 @@ struct Fgk {
         // gradient, slot-form model). The encoder's miss row's sentinel pair (all ones, 0)
         // fails: all ones + 1024 wraps to 1023; the decoder's force makes the limit all ones,
         // above its sentinels (all ones - 1).
-        const uint64_t fail = ballot(kWide ? (w1 <= (w0 | force | (force >> 1))) : (w1 < (nv | force)));
+        const uint64_t fail = ballot(kHuge ? (w1 <= (w0 | fw)) : kWide ? (w1 <= (w0 | force | (force >> 1))) : (w1 < (nv | force)));
         const uint32_t k = ff1(fail);  // 0xFFFFFFFF without a failure: every lane increments
         // lanes below k store: the select runs on a scalar mask (s_bfm_b64), one vector op
         // (measured: an exec-masked store, s_bfm + save/restore of exec, made the encoder 3 %
         // slower than a compare and select)
-        *(lds_u32 *)(size_t)sel(below_mask(k), lds_off(&T.wt[a]), lds_off(scr32())) = nv;
+        *(__attribute__((address_space(3))) Wt *)(size_t)sel(below_mask(k), lds_off(&T.wt[a]), lds_off(scrw())) = nv;
         __builtin_amdgcn_wave_barrier();
         return k;
     }
@@ -690,12 +737,12 @@ struct Fgk {
     // returns the first reported level >= m (0xFFFFFFFF: none, the root lanes bumped the root)
     __device__ __forceinline__ uint32_t update_from(uint32_t a, uint32_t m)
     {
-        const uint32_t w0 = T.wt[a], w1 = T.wt[a + 1];
-        const uint32_t nv = w0 + kInc;
+        const Wt w0 = T.wt[a], w1 = T.wt[a + 1];
+        const Wt nv = w0 + kInc;
         const uint64_t lo = below_mask(m);
         const uint64_t fail = ballot(kWide ? (w1 <= w0) : (w1 < nv)) & ~lo;
         const uint32_t k = ff1(fail);
-        *(lds_u32 *)(size_t)sel(below_mask(k) & ~lo, lds_off(&T.wt[a]), lds_off(scr32())) = nv;
+        *(__attribute__((address_space(3))) Wt *)(size_t)sel(below_mask(k) & ~lo, lds_off(&T.wt[a]), lds_off(scrw())) = nv;
         __builtin_amdgcn_wave_barrier();
         return k;
     }
@@ -898,10 +945,16 @@ struct RecSink {
 
 // --------------------------------------------------------------------------- the encoder --
 
-template <bool kWide, int kSrc>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void encode_kernel(Batch bt)
+// Waves per SIMD each tree layout's LDS admits (8 four-wave workgroups per CU narrow, 6 wide, 4
+// huge): the register budget the compiler may use (fewer scalar spills in the wide kernels,
+// which C4's single long stream runs)
+template <int kW>
+constexpr int kWavesPerSimd = kW == 0 ? 8 : (kW == 1 ? 6 : 4);
+
+template <int kW, int kSrc>
+__global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW>))) void encode_kernel(Batch bt)
 {
-    __shared__ Tree<kWide, false> trees[kWaves];
+    __shared__ Tree<kW, false> trees[kWaves];
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
@@ -915,15 +968,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     const uint64_t out_off = uni64(bt.out_offs[sid]);
     const uint64_t cap = uni64(bt.out_caps[sid]);
 
-    // worst-case symbol count decides narrow / wide; the other variant's launch skips. The wide
-    // tree's 32-bit weights hold any stream below 2^32 - 1 symbols; the count is checked as the
-    // symbols are produced (RLE usually makes far fewer than the worst case).
+    // the worst-case symbol count (MNP-5 expands by at most 4/3) decides the tree layout; the
+    // other layouts' launches skip the stream
     const uint64_t max_sym = kSrc == SRC_SYMBOLS ? n : n + n / 3 + 2;
-    const bool narrow_ok = max_sym <= kNarrowMaxSymbols;
-    if (kWide == narrow_ok) return;
+    if (tree_kind(max_sym, bt.min_tree) != (uint32_t)kW) return;
     const uint32_t window = uni(g_window);
 
-    Fgk<kWide, false> fgk(trees[wv], lane);
+    Fgk<kW, false> fgk(trees[wv], lane);
     RecSink sink;
     sink.rs = make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
     sink.wbase = 0;
@@ -1056,12 +1107,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     };
 
     uint64_t nsym = 0;
-    bool over = false;  // >= 2^32 - 1 symbols: beyond the wide tree's weights
     uint32_t next = buf_load(rin, lane * 4);
     RleCarry cy = {0, 0, 0};
     // Two copies of the chunk loop: streams that fit one window (every batch stream) run without
-    // the window bookkeeping, which would otherwise sit in scalar registers across the hot loop;
-    // only the wide trees can reach 2^32 - 1 symbols.
+    // the window bookkeeping, which would otherwise sit in scalar registers across the hot loop.
     auto chunks = [&](auto windowed) __attribute__((always_inline)) {
         constexpr bool kWin = decltype(windowed)::value;
         for (uint32_t ci = 0; ci < nch && !fgk.bad; ++ci, ioff += 256) {
@@ -1079,10 +1128,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
             next = buf_load(rin, ioff + lane * 4);  // out of range past the end: reads 0
             const uint32_t m = ci + 1 < nch ? 256u : (uint32_t)(n - 256ull * ci);
             if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
-                if (kWide && nsym + m > kWideMaxSymbols) {
-                    over = true;
-                    break;
-                }
                 fgk.T.syms[lane] = chunk;
                 __builtin_amdgcn_wave_barrier();
                 code_all(m);
@@ -1094,10 +1139,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
             const uint32_t ns = rle_chunk<kSrc>(chunk, m, ci + 1 == nch ? 1u : 0u, cy, fgk.T.syms,
                                                 fgk.scr32(), lane);
             HC_PROF_END(4);
-            if (kWide && nsym + ns > kWideMaxSymbols) {
-                over = true;
-                break;
-            }
             code_all(ns);
             nsym += ns;
         }
@@ -1106,14 +1147,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void e
     else chunks(std::true_type{});
 
     const uint64_t total = sink.finish();
-    const uint32_t st = fgk.bad ? (uint32_t)HC_ERR_DEVICE
-                                : (over ? (uint32_t)HC_ERR_UNSUPPORTED : (total <= cap ? 0u : (uint32_t)HC_ERR_CAPACITY));
+    const uint32_t st = fgk.bad ? (uint32_t)HC_ERR_DEVICE : (total <= cap ? 0u : (uint32_t)HC_ERR_CAPACITY);
     // headers.cpp:110-116: u64 little-endian symbol count in words 0-1 (stored after every
     // payload word by program order)
     buf_store(make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)8)), lane < 2 ? lane * 4 : kDrop,
               lane ? (uint32_t)(nsym >> 32) : (uint32_t)nsym);
     if (lane == 0) {
-        bt.out_lens[sid] = (fgk.bad || over) ? 0 : total;
+        bt.out_lens[sid] = fgk.bad ? 0 : total;
         bt.status[sid] = (int32_t)st;
     }
     trace_wave(sid, t0, lane);
@@ -1271,10 +1311,10 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
     return all & 0xFFFFu;
 }
 
-template <bool kWide, int kDst>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void decode_kernel(Batch bt)
+template <int kW, int kDst>
+__global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW>))) void decode_kernel(Batch bt)
 {
-    __shared__ Tree<kWide, true> trees[kWaves];
+    __shared__ Tree<kW, true> trees[kWaves];
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
@@ -1302,19 +1342,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
         // decode, and the reference ends such a stream with status 9 (transform.cpp:394-398)
         if (count > (avail >= 8 ? avail - 7 : 0)) st = HC_ERR_HUFFMAN;
         else if (kDst == DST_RAW && (flags & 0x40u)) st = HC_ERR_UNSUPPORTED;
-        else if (count > kWideMaxSymbols) st = HC_ERR_UNSUPPORTED;
     }
-    const bool narrow_ok = count <= kNarrowMaxSymbols;
-    if (st == 0 && kWide == narrow_ok) return;  // the other variant's launch owns it
+    if (st == 0 && tree_kind(count, bt.min_tree) != (uint32_t)kW) return;  // another layout's launch owns it
     if (st != 0) {
-        if (!kWide && lane == 0) {
+        if (kW == 0 && lane == 0) {
             bt.status[sid] = (int32_t)st;
             bt.out_lens[sid] = 0;
         }
         return;
     }
 
-    Fgk<kWide, true> fgk(trees[wv], lane);
+    Fgk<kW, true> fgk(trees[wv], lane);
     BitSource in;
     in.rs = rin;
     in.ibase = 0;
@@ -1337,7 +1375,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     const uint32_t dmask = kDst == DST_RAW && (flags & 0x80u) ? 255u : 0u;  // diff model
     RevCarry rc = {0, 0, 0};
     uint8_t *const sbuf = reinterpret_cast<uint8_t *>(fgk.T.syms);  // this block's symbols
-    const uint32_t n = (uint32_t)count;
+    // symbol indices: 32-bit below 2^32 symbols (narrow / wide), 64-bit for the huge layout
+    using Idx = std::conditional_t<kW == 2, uint64_t, uint32_t>;
+    const Idx n = (Idx)count;
     // bits read from the stream = words pushed into the window * 32 - bits still in it; the
     // payload starts at bit 72. A stream that ends early decodes zero bits past its end (the
     // range check); the reference stops there with status 9 (transform.cpp:394-398), which is
@@ -1351,7 +1391,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     // that fit one window (input and output), with it for the rest
     auto blocks = [&](auto windowed) __attribute__((always_inline)) {
         constexpr bool kWin = decltype(windowed)::value;
-        for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+        for (Idx i0 = 0; i0 < n; i0 += 256) {
             if (fgk.bad || consumed() > payload_bits + 64) break;
             if constexpr (kWin) {
                 if (in.cbase >= window) {  // slide the input window to the current chunk (a block of
@@ -1368,8 +1408,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                 }
             }
             prio_by_progress(i0, n);
-            const uint32_t i1 = min(n, i0 + 256);
-            uint32_t i = i0;
+            Idx i1;
+            if constexpr (kW == 2) i1 = n - i0 < 256 ? n : i0 + 256;
+            else i1 = min(n, i0 + 256);
+            Idx i = i0;
             while (i < i1) {
                 // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
                 // where the walk from the root stops (depth d <= 8), the levels above give the
@@ -1406,7 +1448,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                 // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
                 // both sign bits set, one scalar AND
                 int32_t left = (int32_t)(i - i1);
-                lds_u8 *so = (lds_u8 *)sbuf + (i - i0);  // the symbol's byte (LDS address in a VGPR)
+                lds_u8 *so = (lds_u8 *)sbuf + (uint32_t)(i - i0);  // the symbol's byte (LDS address in a VGPR)
                 asm("" : "+v"(so));
                 do {
                     const uint32_t e8 = uni(pr);  // the leaf's entry
@@ -1487,7 +1529,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
             }
             __builtin_amdgcn_wave_barrier();
             const uint32_t x4 = fgk.T.syms[lane];
-            const uint32_t m = i1 - i0;
+            const uint32_t m = (uint32_t)(i1 - i0);
             if (kDst == DST_SYMBOLS) {
                 for (uint32_t b = 0; b < 4; ++b)
                     buf_store8(rout, lane * 4 + b < m ? (uint32_t)(pos - obase) + lane * 4 + b : kDrop, byte_of(x4, b));
@@ -1514,37 +1556,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
 
 }  // namespace
 
-hipError_t launch_encode(const Batch &b, EncSrc src, hipStream_t st)
+hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st)
 {
-    if (b.n == 0) return hipSuccess;
+    if (b0.n == 0) return hipSuccess;
+    Batch b = b0;
+    b.min_tree = g_min_tree;
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
+    // one launch per tree layout; each stream is coded by exactly one of them (tree_kind)
     switch (src) {
     case SRC_RAW:
-        encode_kernel<false, SRC_RAW><<<grid, block, 0, st>>>(b);
-        encode_kernel<true, SRC_RAW><<<grid, block, 0, st>>>(b);
+        encode_kernel<0, SRC_RAW><<<grid, block, 0, st>>>(b);
+        encode_kernel<1, SRC_RAW><<<grid, block, 0, st>>>(b);
+        encode_kernel<2, SRC_RAW><<<grid, block, 0, st>>>(b);
         break;
     case SRC_RAW_DIFF:
-        encode_kernel<false, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
-        encode_kernel<true, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
+        encode_kernel<0, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
+        encode_kernel<1, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
+        encode_kernel<2, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
         break;
     default:
-        encode_kernel<false, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
-        encode_kernel<true, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
+        encode_kernel<0, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
+        encode_kernel<1, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
+        encode_kernel<2, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
         break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_decode(const Batch &b, DecDst dst, hipStream_t st)
+hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)
 {
-    if (b.n == 0) return hipSuccess;
+    if (b0.n == 0) return hipSuccess;
+    Batch b = b0;
+    b.min_tree = g_min_tree;
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
     if (dst == DST_RAW) {
-        decode_kernel<false, DST_RAW><<<grid, block, 0, st>>>(b);
-        decode_kernel<true, DST_RAW><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
+        decode_kernel<1, DST_RAW><<<grid, block, 0, st>>>(b);
+        decode_kernel<2, DST_RAW><<<grid, block, 0, st>>>(b);
     } else {
-        decode_kernel<false, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
-        decode_kernel<true, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        decode_kernel<1, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        decode_kernel<2, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
     }
     return hipGetLastError();
 }
@@ -1557,6 +1609,13 @@ extern "C" int hc_debug_set_window(uint32_t bytes)
     uint32_t w = bytes < 4096u ? 4096u : (bytes > (1u << 30) ? (1u << 30) : bytes);
     w &= ~255u;
     return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_window), &w, sizeof(w)) == hipSuccess ? 0 : HC_ERR_DEVICE;
+}
+
+extern "C" int hc_debug_set_min_tree(uint32_t kind)
+{
+    // 0 narrow, 1 wide, 2 huge: the smallest tree layout of every later FGK launch
+    hc::g_min_tree = kind > 2 ? 2 : kind;
+    return 0;
 }
 
 extern "C" int hc_debug_set_trace(void *dev_buf)

@@ -20,6 +20,7 @@ struct Batch {
     uint64_t *out_lens;
     int32_t *status;
     uint32_t flags;  // header flags byte for SRC_SYMBOLS encodes
+    uint32_t min_tree;  // set by the launchers: the smallest FGK tree layout (hc_debug_set_min_tree)
 };
 
 enum EncSrc { SRC_RAW = 0, SRC_RAW_DIFF = 1, SRC_SYMBOLS = 2 };

@@ -290,6 +290,17 @@ def debug_set_window(nbytes):
         raise HCodecError(f"hc_debug_set_window failed: {rc}")
 
 
+def debug_set_min_tree(kind):
+    """Test hook (not part of include/hcodec.h): the smallest FGK tree layout every later launch
+    in this process may use (0 narrow, 1 wide, 2 huge: 64-bit weights), so that small streams
+    exercise the kernels otherwise reserved for streams of > 2^22 - 2 / >= 2^32 - 1 symbols."""
+    f = lib().hc_debug_set_min_tree
+    f.argtypes = [ctypes.c_uint32]
+    rc = f(int(kind))
+    if rc:
+        raise HCodecError(f"hc_debug_set_min_tree failed: {rc}")
+
+
 def compress_bound(n, use_adapt=False):
     return int(lib().hc_compress_bound(n, int(bool(use_adapt))))
 

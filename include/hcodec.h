@@ -38,7 +38,8 @@ enum hc_status {
     HC_ERR_LEFTOVER = 15,     /* transform.cpp:354-358  bytes left after the last block      */
     /* beyond the reference (it has no equivalent, or crashes) */
     HC_ERR_CAPACITY = 64,     /* output capacity too small; the needed length is reported    */
-    HC_ERR_UNSUPPORTED = 65,  /* >= 2^32-1 FGK symbols in one stream (32-bit tree weights) */
+    HC_ERR_UNSUPPORTED = 65,  /* -a stream given to a non-adaptive entry point or vice versa; an
+                                 adaptive matrix whose block RLE holds >= 2^32-1 symbols     */
     HC_ERR_BLOCK_SIZE = 66,   /* forged adaptive header, block size 0 (reference: SIGFPE)    */
     HC_ERR_TOO_LARGE = 67,    /* forged adaptive header, W*H > 2^36 (reference: bad_alloc)   */
     HC_ERR_DEVICE = 70,       /* HIP runtime error / no gfx950 device                        */

@@ -9,7 +9,7 @@ launches = collections.defaultdict(set)  # per (kernel, pass): dispatches, to re
 for f in glob.glob(os.path.join(base, f'{tag}_pmc_*', '*counter_collection.csv')):
     for r in csv.DictReader(open(f)):
         k = r['Kernel_Name']
-        if 'encode_kernel<false' in k or 'decode_kernel<false' in k:
+        if any(t in k for t in ('encode_kernel<false', 'decode_kernel<false', 'encode_kernel<0', 'decode_kernel<0')):
             kk = 'encode' if 'encode_kernel' in k else 'decode'
             agg[kk][r['Counter_Name']] += float(r['Counter_Value'])
             launches[(kk, r['Counter_Name'])].add(r['Dispatch_Id'])

@@ -30,9 +30,10 @@ FGK_SRC = os.path.join(ROOT, "huffman-codec_amd", "csrc", "hc_fgk.hip")
 
 
 def kernel_key(name):
-    """encode_kernel<false, 1> -> ('encode_kernel', narrow)"""
-    m = re.search(r"(encode_kernel|decode_kernel)<(false|true), (\d)>", name)
-    return (m.group(1), m.group(2) == "false", int(m.group(3))) if m else None
+    """encode_kernel<0, 1> (tree layout 0 = narrow; round-1 builds: <false, 1>) ->
+    ('encode_kernel', narrow, source / destination kind)"""
+    m = re.search(r"(encode_kernel|decode_kernel)<(false|true|\d), (\d)>", name)
+    return (m.group(1), m.group(2) in ("false", "0"), int(m.group(3))) if m else None
 
 
 def main():

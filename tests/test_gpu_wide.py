@@ -3,7 +3,7 @@
 The kernels switch to the 32-bit weight layout ("wide") once a stream can exceed 2^22 - 2
 symbols: the encoder for raw inputs over ~3.1 MB (n + n/3 + 2 > 2^22 - 2), the decoder for
 counts over 2^22 - 2 (hc_fgk.hip: encode_kernel / decode_kernel). These inputs are the only
-ones that reach encode_kernel<true, SRC_RAW | SRC_RAW_DIFF> and decode_kernel<true, DST_RAW>;
+ones that reach encode_kernel<1, SRC_RAW | SRC_RAW_DIFF> and decode_kernel<1, DST_RAW>;
 their outputs are compared with the reference binary's digests (tests/golden/digests.json
 "wide", made by tests/golden/make_golden_wide.py from oracle/_ref/huffman-codec-O2):
 
