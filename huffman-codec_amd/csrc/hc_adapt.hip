@@ -36,10 +36,28 @@
 //   undiff    per 16 KB chunk: byte sums, a per-stream scan of them, byte prefix sums.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "hc_internal.h"
 
 namespace hc {
 namespace {
+
+// Diagnostic build (-DHC_TC_PROF): tile_cost_kernel sums the s_memtime cycles of its phases
+// (load, equality words, candidates, summaries) into g_tc_prof (hc_debug_tc_prof reads it).
+#ifdef HC_TC_PROF
+__device__ unsigned long long g_tc_prof[4];
+#define HC_TC_BEGIN() uint64_t tc_t = __builtin_amdgcn_s_memtime()
+#define HC_TC_MARK(i)                                                                              \
+    do {                                                                                           \
+        const uint64_t tc_n = __builtin_amdgcn_s_memtime();                                        \
+        if (tid == 0) atomicAdd(&g_tc_prof[(i) - 1], (unsigned long long)(tc_n - tc_t));           \
+        tc_t = tc_n;                                                                               \
+    } while (0)
+#else
+#define HC_TC_BEGIN()
+#define HC_TC_MARK(i)
+#endif
 
 constexpr uint32_t kTile = 128;
 constexpr uint32_t kCand = 8;        // B = 8 << c, c = 0..7 (transform.cpp:294-328, <= 7 doublings)
@@ -117,6 +135,16 @@ Ws carve(void *work, uint64_t bytes, uint32_t n)
 
 // --------------------------------------------------------------------- wave / WG helpers ---
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads and stores (__syncthreads' release fence would drain those too, so a tile
+// prefetched into registers or cost words just stored would stall every barrier).
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint64_t lanes_below(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -154,8 +182,11 @@ __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l)
 }
 
 // index i with pre[i] <= t < pre[i + 1] (pre[0] = 0, pre[n] = total, t < total)
-__device__ __forceinline__ uint32_t find_item(const uint64_t *pre, uint32_t n, uint64_t t)
+// per: every item's count when they are all equal (the plan kernels store it in ctr[8 + column];
+// ~0 otherwise): then a division replaces the binary search's dependent loads
+__device__ __forceinline__ uint32_t find_item(const uint64_t *pre, uint32_t n, uint64_t t, uint64_t per)
 {
+    if (per != ~0ull && per != 0) return (uint32_t)(t / per);
     uint32_t lo = 0, hi = n;  // pre[lo] <= t < pre[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -166,22 +197,31 @@ __device__ __forceinline__ uint32_t find_item(const uint64_t *pre, uint32_t n, u
 }
 
 // Exclusive scans of kC columns over n items in ONE workgroup of 1024 threads. need(i, v) fills
-// the item's values; put(i, base) receives its exclusive prefix; tot[] the totals.
+// the item's values; put(i, base) receives its exclusive prefix; tot[] the totals; uni[] each
+// column's common value when every item has the same, else ~0 (find_item's fast path).
 template <int kC, class Need, class Put>
-__device__ void wg_scan(uint32_t n, Need need, Put put, uint64_t *tot)
+__device__ void wg_scan(uint32_t n, Need need, Put put, uint64_t *tot, uint64_t *uni = nullptr)
 {
     __shared__ uint64_t part[1024][kC];
+    __shared__ uint32_t same[kC];
     const uint32_t t = threadIdx.x, per = (n + 1023) / 1024;
     const uint32_t b = t * per, e = b + per < n ? b + per : n;
-    uint64_t s[kC];
+    uint64_t s[kC], v0[kC];
     for (int c = 0; c < kC; ++c) s[c] = 0;
+    if (t < kC) same[t] = 1;
+    if (n) need(0, v0);
+    __syncthreads();
     for (uint32_t i = b; i < e; ++i) {
         uint64_t v[kC];
         need(i, v);
-        for (int c = 0; c < kC; ++c) s[c] += v[c];
+        for (int c = 0; c < kC; ++c) {
+            s[c] += v[c];
+            if (v[c] != v0[c]) same[c] = 0;
+        }
     }
     for (int c = 0; c < kC; ++c) part[t][c] = s[c];
     __syncthreads();
+    if (uni && t < kC) uni[t] = (n && same[t]) ? v0[t] : ~0ull;
     if (t < kC) {  // one thread per column: sequential scan of 1024 partials
         uint64_t acc = 0;
         for (uint32_t k = 0; k < 1024; ++k) {
@@ -402,13 +442,14 @@ __global__ __launch_bounds__(1024) void enc_plan_kernel(EncArgs a, Ws ws)
         ws.idx[1][i] = base[1];
         ws.idx[2][i] = base[2];
     };
-    __shared__ uint64_t tot[4];
-    wg_scan<4>(a.n, need, put, tot);
+    __shared__ uint64_t tot[4], uni[4];
+    wg_scan<4>(a.n, need, put, tot, uni);
     if (threadIdx.x == 0) {
-        for (int k = 0; k < 3; ++k) ws.idx[k][a.n] = tot[k];
-        ws.ctr[0] = tot[0];
-        ws.ctr[1] = tot[1];
-        ws.ctr[2] = tot[2];
+        for (int k = 0; k < 3; ++k) {
+            ws.idx[k][a.n] = tot[k];
+            ws.ctr[k] = tot[k];
+            ws.ctr[8 + k] = uni[k];
+        }
     }
 }
 
@@ -433,6 +474,17 @@ __device__ __forceinline__ uint32_t load4(const uint8_t *m, int64_t lin, uint64_
     return v;
 }
 
+// 0x80 in every byte of x that is zero
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x)
+{
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+// bit q (0..3): byte q of a equals byte q of b (the four flags gathered by one multiply)
+__device__ __forceinline__ uint32_t eq_nibble(uint32_t a, uint32_t b)
+{
+    return (((zero_bytes(a ^ b) >> 7) * 0x204081u) >> 21) & 0xFu;
+}
+
 // bytewise a - b and a + b (mod 256 per byte)
 __device__ __forceinline__ uint32_t sub8(uint32_t a, uint32_t b)
 {
@@ -445,11 +497,17 @@ __device__ __forceinline__ uint32_t add8(uint32_t a, uint32_t b)
 
 // The tile's rows ty0 - 1 .. ty0 + th - 1, bytes tx0 - 4 .. tx0 + tw - 1, as dwords (coalesced
 // along each row; all of a thread's loads issue before its LDS stores), diff model applied
-// (transform.cpp:220-229: d[k] = m[k] - m[k-1] over the linear matrix, m[-1] = 0).
+// (transform.cpp:220-229: d[k] = m[k] - m[k-1] over the linear matrix, m[-1] = 0). Only byte 3
+// of a row's first dword (x = tx0 - 1) is ever read, so its own previous byte is not needed.
+// Dword-aligned rows (aligned matrix, W % 4 == 0: every 512-wide batch) take one aligned load per
+// dword; the diff model's previous byte is the top byte of the dword before, which the lane
+// below loaded (wave_shr 1; lane 0 loads it again).
 __device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64_t n, uint64_t W, uint64_t tx0,
                                           uint64_t ty0, uint32_t tw, uint32_t th, bool diff, uint32_t tid)
 {
     const uint32_t nd = (tw + 7) / 4, items = (th + 1) * nd;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(mat) | W) & 3) == 0;
+    const uint32_t lane = tid & 63;
     constexpr int kU = 4;
     for (uint32_t base = 0; base < items; base += 256 * kU) {
         uint32_t v[kU], pv[kU];
@@ -459,8 +517,17 @@ __device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64
             const uint32_t r = it / nd, d = it - r * nd;
             const int64_t lin = (int64_t)(ty0 + r) * (int64_t)W - (int64_t)W + (int64_t)tx0 - 4 + 4 * (int64_t)d;
             const bool on = it < items && (r > 0 || ty0 > 0);
-            v[u] = on ? load4(mat, lin, n) : 0u;
-            pv[u] = on && diff ? load4(mat, lin - 1, n) : 0u;
+            if (aligned) {
+                const bool whole = on && lin >= 0 && (uint64_t)lin + 4 <= n;
+                v[u] = whole ? *reinterpret_cast<const uint32_t *>(mat + lin) : (on ? load4(mat, lin, n) : 0u);
+                const uint32_t below = lane_shr1(v[u], 0u);
+                const bool own = on && diff && lane == 0 && d > 0;
+                pv[u] = own ? load4(mat, lin - 4, n) : below;  // the dword before (d > 0)
+                pv[u] = (pv[u] >> 24) | (v[u] << 8);         // bytes lin - 1 .. lin + 2
+            } else {
+                v[u] = on ? load4(mat, lin, n) : 0u;
+                pv[u] = on && diff ? load4(mat, lin - 1, n) : 0u;
+            }
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -473,7 +540,104 @@ __device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64
     }
 }
 
-__global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
+// (row, dword) of the items tid, tid + 256, tid + 512, ... of a tile image nd dwords wide,
+// stepped without a division per item
+struct TileWalk {
+    uint32_t r, d, q, rem, nd;
+    __device__ __forceinline__ TileWalk(uint32_t nd_, uint32_t tid) : nd(nd_)
+    {
+        r = tid / nd;
+        d = tid - r * nd;
+        q = 256 / nd;
+        rem = 256 - q * nd;
+    }
+    __device__ __forceinline__ void next()
+    {
+        d += rem;
+        r += q;
+        if (d >= nd) {
+            d -= nd;
+            ++r;
+        }
+    }
+};
+
+// A tile of the work list (one workgroup's unit in tile_cost / emit_tile): its matrix and place.
+struct TileAt {
+    uint32_t i;            // matrix
+    bool ok;               // the matrix is valid (status 0)
+    uint64_t W, H, tx0, ty0, n;
+    uint32_t tw, th;
+    const uint8_t *mat;
+};
+__device__ __forceinline__ TileAt tile_at(const EncArgs &a, const Ws &ws, uint64_t t)
+{
+    TileAt g;
+    g.i = find_item(ws.idx[0], a.n, t, ws.ctr[8 + 0]);
+    const AMeta &M = ws.meta[g.i];
+    g.ok = M.status == 0;
+    g.W = M.w;
+    g.H = M.h;
+    g.n = M.w * M.h;
+    const uint64_t ntx = cdiv(g.W, kTile), local = t - ws.idx[0][g.i];
+    g.tx0 = (local % ntx) * kTile;
+    g.ty0 = (local / ntx) * kTile;
+    g.tw = (uint32_t)(g.W - g.tx0 < kTile ? g.W - g.tx0 : kTile);
+    g.th = (uint32_t)(g.H - g.ty0 < kTile ? g.H - g.ty0 : kTile);
+    g.mat = a.in + a.in_offs[g.i];
+    return g;
+}
+
+// The tile image of load_tile in two halves, so that a workgroup can fetch its next tile into
+// registers while it works on the current one: tile_fetch issues the (raw) dword loads, one
+// item per thread and u (the rows' (kTile + 8) / 4 dwords x kTile + 1 rows <= kLU x 256);
+// tile_put stores them and applies the diff model in LDS (each dword's previous byte is the
+// byte before it in the row image; a row's first dword needs only its own byte 2 for byte 3).
+constexpr uint32_t kLU = ((kTile + 1) * ((kTile + 8) / 4) + 255) / 256;
+__device__ __forceinline__ void tile_fetch(const TileAt &g, uint32_t *v, uint32_t tid)
+{
+    const uint32_t nd = (g.tw + 7) / 4, items = (g.th + 1) * nd;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(g.mat) | g.W) & 3) == 0;
+    TileWalk wk(nd, tid);
+#pragma unroll
+    for (uint32_t u = 0; u < kLU; ++u, wk.next()) {
+        const uint32_t it = u * 256 + tid;
+        const uint32_t r = wk.r, d = wk.d;
+        const int64_t lin = (int64_t)(g.ty0 + r) * (int64_t)g.W - (int64_t)g.W + (int64_t)g.tx0 - 4 + 4 * (int64_t)d;
+        const bool on = it < items && (r > 0 || g.ty0 > 0);
+        const bool whole = on && aligned && lin >= 0 && (uint64_t)lin + 4 <= g.n;
+        v[u] = whole ? *reinterpret_cast<const uint32_t *>(g.mat + lin) : (on ? load4(g.mat, lin, g.n) : 0u);
+    }
+}
+__device__ __forceinline__ void tile_put(uint8_t *D, const TileAt &g, uint32_t *v, bool diff, uint32_t tid)
+{
+    const uint32_t nd = (g.tw + 7) / 4, items = (g.th + 1) * nd;
+    uint32_t at[kLU];  // the items' LDS byte offsets (kDS * r + 4 d), or ~0 past the image
+    {
+        TileWalk wk(nd, tid);
+#pragma unroll
+        for (uint32_t u = 0; u < kLU; ++u, wk.next())
+            at[u] = u * 256 + tid < items ? wk.r * kDS + 4 * wk.d : ~0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kLU; ++u)
+        if (at[u] != ~0u) *reinterpret_cast<uint32_t *>(D + at[u]) = v[u];
+    lds_barrier();
+    if (!diff) return;
+#pragma unroll
+    for (uint32_t u = 0; u < kLU; ++u) {
+        // a row's first dword (at % kDS == 0) needs no byte before it (only its byte 3 is read)
+        const uint32_t pb = (at[u] != ~0u && at[u] % kDS != 0) ? D[at[u] - 1] : 0u;
+        v[u] = sub8(v[u], (v[u] << 8) | pb);
+    }
+    lds_barrier();
+#pragma unroll
+    for (uint32_t u = 0; u < kLU; ++u)
+        if (at[u] != ~0u) *reinterpret_cast<uint32_t *>(D + at[u]) = v[u];
+    lds_barrier();
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_cost_kernel(EncArgs a, Ws ws)
 {
     __shared__ uint8_t D[(kTile + 1) * kDS];  // DT(r, xl): y = ty0 + r - 1, x = tx0 + xl
     __shared__ uint64_t E[4 * kTile];         // Eh[r][2] then Ev[c][2]
@@ -482,60 +646,89 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
     __shared__ uint32_t red[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[0];
+    const bool diff = a.diff != 0;
+    // the next tile's raw dwords are in flight while this one is worked on
+    uint32_t v[kLU];
+    TileAt nx;
+    if (blockIdx.x < ntiles) {
+        nx = tile_at(a, ws, blockIdx.x);
+        if (nx.ok) tile_fetch(nx, v, tid);
+    }
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t i = find_item(ws.idx[0], a.n, t);
+        const TileAt g = nx;
+        const uint32_t i = g.i;
         AMeta &M = ws.meta[i];
-        if (M.status) continue;  // (uniform over the workgroup)
-        const uint64_t W = M.w, H = M.h;
-        const uint64_t ntx = cdiv(W, kTile), local = t - ws.idx[0][i];
-        const uint64_t tx0 = (local % ntx) * kTile, ty0 = (local / ntx) * kTile;
-        const uint32_t tw = (uint32_t)(W - tx0 < kTile ? W - tx0 : kTile);
-        const uint32_t th = (uint32_t)(H - ty0 < kTile ? H - ty0 : kTile);
-        const uint8_t *mat = a.in + a.in_offs[i];
-        const bool diff = a.diff != 0;
+        HC_TC_BEGIN();
         // 1. the tile plus one row above and one column to the left, diff model applied
-        load_tile(D, mat, M.w * M.h, W, tx0, ty0, tw, th, diff, tid);
-        __syncthreads();
+        if (g.ok) tile_put(D, g, v, diff, tid);
+        if (t + gridDim.x < ntiles) {
+            nx = tile_at(a, ws, t + gridDim.x);
+            if (nx.ok) tile_fetch(nx, v, tid);
+        }
+        if (!g.ok) continue;  // (uniform over the workgroup)
+        const uint64_t W = g.W, H = g.H, tx0 = g.tx0, ty0 = g.ty0;
+        const uint64_t ntx = cdiv(W, kTile);
+        const uint32_t tw = g.tw, th = g.th;
+        HC_TC_MARK(1);
         // 2. Eh[r][k] bit j: x = tx0 + 64k + j equals x - 1 (row ty0 + r); Ev[c][k] bit j: y = ty0 +
-        //    64k + j equals y - 1 (column tx0 + c). One ballot per word; lane k keeps word k.
+        //    64k + j equals y - 1 (column tx0 + c). Eh: one word per thread from 16 dwords of its row
+        //    (SWAR equality nibbles); Ev: lane = row, 4 ballots per dword column.
         {
-            const uint32_t nh = 2 * th, total = nh + 2 * tw;
-            for (uint32_t q0 = 64 * wv; q0 < total; q0 += 256) {
-                uint64_t keep = 0;
-                const uint32_t cnt = total - q0 < 64 ? total - q0 : 64;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    const uint32_t q = q0 + k;
-                    bool e;
-                    if (q < nh) {
-                        const uint32_t rr = q >> 1, col = 64 * (q & 1) + lane;
-                        e = col < tw && tx0 + col > 0 &&
-                            DT(rr + 1, col) == DT(rr + 1, (int)col - 1);
-                    } else {
-                        const uint32_t cc = (q - nh) >> 1, row = 64 * ((q - nh) & 1) + lane;
-                        e = row < th && ty0 + row > 0 && DT(row + 1, cc) == DT(row, cc);
-                    }
-                    const uint64_t b = ballot(e);
-                    keep = lane == k ? b : keep;
+            const uint32_t r = tid >> 1, k = tid & 1;
+            uint64_t word = 0;
+            if (r < th) {
+                const uint8_t *row = D + (r + 1) * kDS + 4 + 64 * k;  // DT(r + 1, 64 k)
+                uint32_t prev = *reinterpret_cast<const uint32_t *>(row - 4);
+                uint32_t lo = 0, hi = 0;
+#pragma unroll
+                for (uint32_t m = 0; m < 16; ++m) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t *>(row + 4 * m);
+                    const uint32_t nib = eq_nibble(w, (w << 8) | (prev >> 24));
+                    if (m < 8) lo |= nib << (4 * m);
+                    else hi |= nib << (4 * (m - 8));
+                    prev = w;
                 }
-                if (lane < cnt) {
-                    const uint32_t q = q0 + lane;
-                    E[q < nh ? q : 2 * kTile + (q - nh)] = keep;
+                word = (uint64_t)hi << 32 | lo;
+                const uint32_t valid = tw > 64 * k ? tw - 64 * k : 0u;  // columns inside the tile
+                word &= valid >= 64 ? ~0ull : ((1ull << valid) - 1);
+                if (tx0 == 0 && k == 0) word &= ~1ull;  // x = 0 has no left neighbour
+            }
+            E[2 * r + k] = word;
+            const uint32_t kk = wv & 1, y = 64 * kk + lane;
+            const bool yok = y < th && ty0 + y > 0;
+            uint64_t keep = 0;
+#pragma unroll 4
+            for (uint32_t dd = 0; dd < 16; ++dd) {
+                const uint32_t d = 16 * (wv >> 1) + dd;
+                const uint32_t a = *reinterpret_cast<const uint32_t *>(D + (y + 1) * kDS + 4 + 4 * d);
+                const uint32_t b = *reinterpret_cast<const uint32_t *>(D + y * kDS + 4 + 4 * d);
+                const uint32_t z = yok ? zero_bytes(a ^ b) : 0u;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint64_t bq = ballot((z >> (8 * q + 7)) & 1u);
+                    keep = lane == 4 * dd + q ? bq : keep;
                 }
             }
+            const uint32_t c = 64 * (wv >> 1) + lane;  // lane L kept column 4 (16 (wv >> 1) + L / 4) + L % 4
+            E[2 * kTile + 2 * c + kk] = c < tw ? keep : 0ull;
         }
-        __syncthreads();
+        lds_barrier();
         const uint64_t *Eh = E, *Ev = E + 2 * kTile;
+        HC_TC_MARK(2);
         // 3. blocks of B <= 128, both scan orders
+        //    (one copy per candidate: B, the lines per word and the group sizes are constants, so
+        //    each thread's LDS reads unroll and issue together)
         const uint32_t nct = M.nc < kTileCand ? M.nc : kTileCand;
-        for (uint32_t c = 0; c < nct; ++c) {
-            const uint32_t B = 8u << c, lg = 3 + c;
+        auto candidate = [&](auto cc) __attribute__((always_inline)) {
+            constexpr uint32_t c = decltype(cc)::value;
+            constexpr uint32_t B = 8u << c, lg = 3 + c;
             const uint32_t nbx = (tw + B - 1) >> lg, nby = (th + B - 1) >> lg;
             const uint32_t per_o = (nbx * nby) << lg, items = 2 * per_o;
             const bool full = (tw & (B - 1)) == 0 && (th & (B - 1)) == 0;
             // whole blocks: one 64-element word of the block's scan per lane (64 / B block rows or
             // columns, B = 128: half of one), first bits substituted, so a block of B = 8 is one
             // leaf and no join; 2 (h, v) x tw x th / 64 items
-            const uint32_t lwpb = lg <= 3 ? 0u : 2 * lg - 6;  // log2 of the words per block
+            constexpr uint32_t lwpb = lg <= 3 ? 0u : 2 * lg - 6;  // log2 of the words per block
             const uint32_t nwords = (tw * th) >> 6;
             for (uint32_t base = 0; full && base < 2 * nwords; base += 256) {
                 const uint32_t it = base + tid;
@@ -547,9 +740,11 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                 if (it < 2 * nwords) {
                     const uint64_t *E2 = o ? Ev : Eh;
                     const uint32_t l0 = o ? x0 : y0, c0 = o ? y0 : x0;  // first line, offset in it
-                    if (B <= 64) {
-                        const uint32_t lpw = 64 >> lg, r0 = j * lpw;
-                        const uint64_t msk = B >= 64 ? ~0ull : (1ull << B) - 1;
+                    if constexpr (B <= 64) {
+                        constexpr uint32_t lpw = 64 >> lg;
+                        const uint32_t r0 = j * lpw;
+                        constexpr uint64_t msk = B >= 64 ? ~0ull : (1ull << (B & 63)) - 1;
+#pragma unroll
                         for (uint32_t q = 0; q < lpw; ++q) {
                             const uint32_t r = r0 + q;
                             uint64_t bits = (E2[2 * (l0 + r) + (c0 >> 6)] >> (c0 & 63)) & msk & ~1ull;
@@ -558,7 +753,7 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                                                   : DT(y0 + r + 1, x0) == DT(y0 + r, x0 + B - 1);
                                 bits |= eq;
                             }
-                            word |= bits << (q * B);
+                            word |= bits << ((q * B) & 63);
                         }
                     } else {  // B = 128 (x0 = y0 = 0): word j = half j & 1 of line j >> 1
                         const uint32_t r = j >> 1;
@@ -606,12 +801,12 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                     part[wv] = s;
                 }
             }
-            __syncthreads();
+            lds_barrier();
             if (B == 128 && tid < 2)
                 hv[tid][0] = full ? seg_cost(seg_join(seg_join(part[4 * tid], part[4 * tid + 1]),
                                                       seg_join(part[4 * tid + 2], part[4 * tid + 3])))
                                   : seg_cost(seg_join(part[2 * tid], part[2 * tid + 1]));
-            __syncthreads();
+            lds_barrier();
             // transform.cpp:113-123: the shorter scan, ties horizontal; word = cost | h << 31
             const uint32_t nblk = nbx * nby;
             const uint64_t per_row = cdiv(W, B);
@@ -624,9 +819,15 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
             }
             for (uint32_t d = 32; d; d >>= 1) sum += __shfl_down(sum, d, 64);
             if (lane == 0) red[wv] = sum;
-            __syncthreads();
+            lds_barrier();
             if (tid == 0) atomicAdd(&M.total[c], (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
-        }
+        };
+        if (nct > 0) candidate(std::integral_constant<uint32_t, 0>{});
+        if (nct > 1) candidate(std::integral_constant<uint32_t, 1>{});
+        if (nct > 2) candidate(std::integral_constant<uint32_t, 2>{});
+        if (nct > 3) candidate(std::integral_constant<uint32_t, 3>{});
+        if (nct > 4) candidate(std::integral_constant<uint32_t, 4>{});
+        HC_TC_MARK(3);
         // 4. tile summaries for the blocks of B >= 256
         if (M.nc > kTileCand) {
             const uint64_t nty = cdiv(H, kTile);
@@ -648,7 +849,8 @@ __global__ __launch_bounds__(256) void tile_cost_kernel(EncArgs a, Ws ws)
                     piece_pack(s, (uint32_t)(w[0] & 1), DT(1, x), DT(th, x));
             }
         }
-        __syncthreads();
+        lds_barrier();
+        HC_TC_MARK(4);
     }
 }
 
@@ -657,10 +859,10 @@ __device__ __forceinline__ Seg seg_block(Seg s, Seg *part, uint32_t tid)
 {
     s = seg_group(s, 64, tid & 63);
     if ((tid & 63) == 0) part[tid >> 6] = s;
-    __syncthreads();
+    lds_barrier();
     Seg r = seg_id();
     if (tid == 0) r = seg_join(seg_join(part[0], part[1]), seg_join(part[2], part[3]));
-    __syncthreads();
+    lds_barrier();
     return r;
 }
 
@@ -671,7 +873,7 @@ __global__ __launch_bounds__(256) void big_cost_kernel(EncArgs a, Ws ws)
     const uint32_t tid = threadIdx.x;
     const uint64_t items = ws.ctr[1];
     for (uint64_t t = blockIdx.x; t < items; t += gridDim.x) {
-        const uint32_t i = find_item(ws.idx[1], a.n, t);
+        const uint32_t i = find_item(ws.idx[1], a.n, t, ws.ctr[8 + 1]);
         AMeta &M = ws.meta[i];
         if (M.status) continue;
         uint64_t k = t - ws.idx[1][i];
@@ -839,7 +1041,7 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[0];
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t i = find_item(ws.idx[0], a.n, t);
+        const uint32_t i = find_item(ws.idx[0], a.n, t, ws.ctr[8 + 0]);
         const AMeta &M = ws.meta[i];
         if (M.status || M.B > kTile) continue;  // (uniform over the workgroup)
         const uint64_t W = M.w, H = M.h, B = M.B;
@@ -848,7 +1050,7 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
         const uint32_t tw = (uint32_t)(W - tx0 < kTile ? W - tx0 : kTile);
         const uint32_t th = (uint32_t)(H - ty0 < kTile ? H - ty0 : kTile);
         load_tile(D, a.in + a.in_offs[i], W * H, W, tx0, ty0, tw, th, a.diff != 0, tid);
-        __syncthreads();
+        lds_barrier();
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
         const uint32_t *offw = at<uint32_t>(ws, M.cost0[M.best]);
         const uint32_t b32 = (uint32_t)B;
@@ -869,7 +1071,7 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
             };
             emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + offw[k], lane);
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -879,7 +1081,7 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EncArgs a, Ws ws)
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const uint64_t items = ws.ctr[1];
     for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
-        const uint32_t i = find_item(ws.idx[1], a.n, t);
+        const uint32_t i = find_item(ws.idx[1], a.n, t, ws.ctr[8 + 1]);
         const AMeta &M = ws.meta[i];
         if (M.status || M.B <= kTile) continue;
         uint64_t k = t - ws.idx[1][i];
@@ -1056,12 +1258,13 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
         ws.idx[1][i] = base[1];
         ws.idx[2][i] = base[2];
     };
-    __shared__ uint64_t tot[3];
-    wg_scan<3>(a.n, need, put, tot);
+    __shared__ uint64_t tot[3], uni[3];
+    wg_scan<3>(a.n, need, put, tot, uni);
     if (threadIdx.x == 0) {
         for (int k = 0; k < 3; ++k) {
             ws.idx[k][a.n] = tot[k];
             ws.ctr[k] = tot[k];
+            ws.ctr[8 + k] = uni[k];
         }
     }
 }
@@ -1288,7 +1491,7 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[2];
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t i = find_item(ws.idx[2], a.n, t);
+        const uint32_t i = find_item(ws.idx[2], a.n, t, ws.ctr[8 + 2]);
         const AMeta &M = ws.meta[i];
         if (M.status || M.mode != 0) continue;  // (uniform over the workgroup)
         const uint64_t W = M.w, H = M.h, B = M.B;
@@ -1318,7 +1521,7 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
                 pos = revert_block(sym, pos, M.count, (uint64_t)sx * sy, place, lane);
             }
         }
-        __syncthreads();
+        lds_barrier();
         uint8_t *mat = a.out + a.out_offs[i];
         const uint32_t nd = (tw + 3) / 4;
         for (uint32_t it = tid; it < th * nd; it += 256) {
@@ -1332,7 +1535,7 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
                 for (uint32_t k = 0; 4 * d + k < tw; ++k) dst[k] = (uint8_t)(v >> (8 * k));
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -1342,7 +1545,7 @@ __global__ __launch_bounds__(256) void unblock_kernel(DecArgs a, Ws ws)
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const uint64_t items = ws.ctr[0];
     for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
-        const uint32_t i = find_item(ws.idx[0], a.n, t);
+        const uint32_t i = find_item(ws.idx[0], a.n, t, ws.ctr[8 + 0]);
         const AMeta &M = ws.meta[i];
         if (M.status || M.mode == 0) continue;
         const uint64_t g = t - ws.idx[0][i];
@@ -1376,7 +1579,7 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(DecArgs a, Ws ws)
     const uint32_t tid = threadIdx.x;
     const uint64_t items = ws.ctr[1];
     for (uint64_t t = blockIdx.x; t < items; t += gridDim.x) {
-        const uint32_t i = find_item(ws.idx[1], a.n, t);
+        const uint32_t i = find_item(ws.idx[1], a.n, t, ws.ctr[8 + 1]);
         const AMeta &M = ws.meta[i];
         const uint64_t c = t - ws.idx[1][i], n = M.w * M.h;
         const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
@@ -1389,9 +1592,9 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(DecArgs a, Ws ws)
         }
         for (uint32_t d = 32; d; d >>= 1) s += __shfl_down(s, d, 64);
         if ((tid & 63) == 0) red[tid >> 6] = s;
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) at<uint8_t>(ws, M.csum)[c] = (uint8_t)(red[0] + red[1] + red[2] + red[3]);
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -1422,7 +1625,7 @@ __global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t items = ws.ctr[1];
     for (uint64_t t = blockIdx.x; t < items; t += gridDim.x) {
-        const uint32_t i = find_item(ws.idx[1], a.n, t);
+        const uint32_t i = find_item(ws.idx[1], a.n, t, ws.ctr[8 + 1]);
         const AMeta &M = ws.meta[i];
         const uint64_t c = t - ws.idx[1][i], n = M.w * M.h;
         const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
@@ -1445,7 +1648,7 @@ __global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
         }
         const uint32_t acc = wave_sum_incl(run);  // the threads' totals (mod 256)
         if (lane == 63) part[wv] = acc;
-        __syncthreads();
+        lds_barrier();
         uint32_t carry = at<uint8_t>(ws, M.csum)[c] + acc - run;
         for (uint32_t k = 0; k < wv; ++k) carry += part[k];
         carry = (carry & 0xFFu) * 0x01010101u;
@@ -1457,7 +1660,7 @@ __global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
             else
                 for (uint64_t q = o; q < e; ++q) mat[q] = (uint8_t)(v >> (8 * (q - o)));
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -1551,3 +1754,15 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
 }
 
 }  // namespace hc
+
+#ifdef HC_TC_PROF
+extern "C" int hc_debug_tc_prof(unsigned long long *out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_tc_prof), sizeof(unsigned long long) * 4) != hipSuccess) return 70;
+    if (reset) {
+        unsigned long long z[4] = {0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_tc_prof), z, sizeof(z)) != hipSuccess) return 70;
+    }
+    return 0;
+}
+#endif
