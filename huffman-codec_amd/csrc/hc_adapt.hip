@@ -1451,16 +1451,18 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
 }
 
 // transform.cpp:162-187 for one block by one wave: revert its RLE from symbol `pos` with a
-// fresh machine, 64 symbols per step, handing every output byte (block-relative index q in scan
-// order, value) to place(); returns the block's end. A count repeats the literal before it.
-template <class Place>
-__device__ __forceinline__ uint64_t revert_block(const uint8_t *sym, uint64_t pos, uint64_t count, uint64_t want,
+// fresh machine, 64 symbols per step (read(p): symbol p + lane), handing every output byte
+// (block-relative index q in scan order, value) to place(); returns the block's end. A count
+// repeats the literal before it: literals are placed by their own lanes, each count's run
+// (up to 255 bytes) by the whole wave, 64 bytes at a time.
+template <class Read, class Place>
+__device__ __forceinline__ uint64_t revert_block(Read &&read, uint64_t pos, uint64_t count, uint64_t want,
                                                  Place place, uint32_t lane)
 {
     uint64_t got = 0;
     uint32_t r = 0, last = 0;
     while (got < want && pos < count) {  // (the bounds pass proved the block whole)
-        const uint32_t xs = sym[pos + lane];
+        const uint32_t xs = read(pos);
         const uint32_t pr = lane_shr1(xs, last);
         const uint32_t inc = fsm_scan(xs == pr ? kFsmEq : kFsmNe);
         const uint32_t s = fsm_at(lane_shr1(inc, kFsmId), r);
@@ -1472,8 +1474,14 @@ __device__ __forceinline__ uint64_t revert_block(const uint8_t *sym, uint64_t po
         const uint32_t L = hit ? (uint32_t)__builtin_ctzll(hit) : 63u;  // last lane of this block
         const bool mine = lane <= L;
         const uint64_t q0 = got + acc - len;
-        if (mine)
-            for (uint32_t e = 0; e < len; ++e) place(q0 + e, val);
+        if (mine && len == 1) place(q0, val);
+        for (uint64_t runs = ballot(mine && len > 1); runs; runs &= runs - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(runs);
+            const uint32_t n = readlane(len, l), v = readlane(val, l);
+            const uint64_t b = got + readlane(acc, l) - n;
+            for (uint32_t j0 = 0; j0 < n; j0 += 64)
+                if (j0 + lane < n) place(b + j0 + lane, v);
+        }
         got += readlane(acc, L);
         r = fsm_at(readlane(inc, L), r);
         last = readlane(xs, L);
@@ -1482,12 +1490,52 @@ __device__ __forceinline__ uint64_t revert_block(const uint8_t *sym, uint64_t po
     return pos;
 }
 
+// A wave's window on a symbol stream read in order: the symbols below `hi` (a multiple of 256)
+// sit in a 1 KB LDS ring, the next 256 are in flight in a register (one dword per lane), so the
+// revert's 64-symbol steps read LDS, not HBM.
+struct SymRing {
+    uint8_t *R;
+    const uint32_t *sw;  // the symbols as dwords (the slab is 16-aligned)
+    uint64_t nsym, hi;
+    uint32_t pf, lane;
+    __device__ __forceinline__ uint32_t fetch(uint64_t at) const
+    {
+        const uint64_t o = at + 4 * lane;
+        return o < nsym ? sw[o >> 2] : 0u;  // (a dword starting below nsym: inside the slack)
+    }
+    __device__ __forceinline__ void start(uint64_t pos)
+    {
+        const uint64_t base = pos & ~255ull;
+        uint32_t q[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) q[k] = fetch(base + 256 * k);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            *reinterpret_cast<uint32_t *>(R + ((base + 256 * k + 4 * lane) & 1023)) = q[k];
+        hi = base + 1024;
+        pf = fetch(hi);
+        __builtin_amdgcn_wave_barrier();
+    }
+    // symbol p + lane (p + 64 <= hi afterwards; p >= hi - 1024 by construction)
+    __device__ __forceinline__ uint32_t operator()(uint64_t p)
+    {
+        while (p + 64 > hi) {
+            *reinterpret_cast<uint32_t *>(R + ((hi + 4 * lane) & 1023)) = pf;
+            hi += 256;
+            pf = fetch(hi);
+        }
+        __builtin_amdgcn_wave_barrier();
+        return R[(p + lane) & 1023];
+    }
+};
+
 // transform.cpp:191-216 for blocks of B = 8..128 (mode 0): one workgroup per tile; each wave
 // reverts the blocks of one tile block row (one group: they follow each other in the stream)
 // into an LDS image of the tile, which then leaves as whole rows
 __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
 {
     __shared__ uint8_t T[kTile * kDS];
+    __shared__ uint32_t ring[4][256];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[2];
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -1504,9 +1552,15 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
         const uint32_t *starts = at<uint32_t>(ws, M.starts);
         const uint64_t per_row = cdiv(W, B);
+        SymRing rd;
+        rd.R = reinterpret_cast<uint8_t *>(ring[wv]);
+        rd.sw = reinterpret_cast<const uint32_t *>(sym);
+        rd.nsym = M.count;
+        rd.lane = lane;
         for (uint32_t by = wv; by < nby; by += 4) {
             const uint64_t gby = ty0 / B + by;
             uint64_t pos = starts[gby * ntx + tix];
+            rd.start(pos);
             for (uint32_t bx = 0; bx < nbx; ++bx) {
                 const uint64_t k = gby * per_row + tx0 / B + bx;
                 const uint32_t x0 = bx * b32, y0 = by * b32;
@@ -1518,7 +1572,7 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
                     const uint32_t a1 = div_small((uint32_t)q, inner, inv), b1 = (uint32_t)q - a1 * inner;
                     T[(y0 + (horiz ? a1 : b1)) * kDS + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
                 };
-                pos = revert_block(sym, pos, M.count, (uint64_t)sx * sy, place, lane);
+                pos = revert_block(rd, pos, M.count, (uint64_t)sx * sy, place, lane);
             }
         }
         lds_barrier();
@@ -1566,7 +1620,7 @@ __global__ __launch_bounds__(256) void unblock_kernel(DecArgs a, Ws ws)
                 const uint64_t b1 = q - a1 * inner;
                 mat[(y0 + (horiz ? a1 : b1)) * W + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
             };
-            pos = revert_block(sym, pos, M.count, want, place, lane);
+            pos = revert_block([&](uint64_t p) -> uint32_t { return sym[p + lane]; }, pos, M.count, want, place, lane);
         }
     }
 }
