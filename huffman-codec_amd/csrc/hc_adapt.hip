@@ -495,51 +495,6 @@ __device__ __forceinline__ uint32_t add8(uint32_t a, uint32_t b)
     return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
 }
 
-// The tile's rows ty0 - 1 .. ty0 + th - 1, bytes tx0 - 4 .. tx0 + tw - 1, as dwords (coalesced
-// along each row; all of a thread's loads issue before its LDS stores), diff model applied
-// (transform.cpp:220-229: d[k] = m[k] - m[k-1] over the linear matrix, m[-1] = 0). Only byte 3
-// of a row's first dword (x = tx0 - 1) is ever read, so its own previous byte is not needed.
-// Dword-aligned rows (aligned matrix, W % 4 == 0: every 512-wide batch) take one aligned load per
-// dword; the diff model's previous byte is the top byte of the dword before, which the lane
-// below loaded (wave_shr 1; lane 0 loads it again).
-__device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64_t n, uint64_t W, uint64_t tx0,
-                                          uint64_t ty0, uint32_t tw, uint32_t th, bool diff, uint32_t tid)
-{
-    const uint32_t nd = (tw + 7) / 4, items = (th + 1) * nd;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(mat) | W) & 3) == 0;
-    const uint32_t lane = tid & 63;
-    constexpr int kU = 4;
-    for (uint32_t base = 0; base < items; base += 256 * kU) {
-        uint32_t v[kU], pv[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint32_t it = base + u * 256 + tid;
-            const uint32_t r = it / nd, d = it - r * nd;
-            const int64_t lin = (int64_t)(ty0 + r) * (int64_t)W - (int64_t)W + (int64_t)tx0 - 4 + 4 * (int64_t)d;
-            const bool on = it < items && (r > 0 || ty0 > 0);
-            if (aligned) {
-                const bool whole = on && lin >= 0 && (uint64_t)lin + 4 <= n;
-                v[u] = whole ? *reinterpret_cast<const uint32_t *>(mat + lin) : (on ? load4(mat, lin, n) : 0u);
-                const uint32_t below = lane_shr1(v[u], 0u);
-                const bool own = on && diff && lane == 0 && d > 0;
-                pv[u] = own ? load4(mat, lin - 4, n) : below;  // the dword before (d > 0)
-                pv[u] = (pv[u] >> 24) | (v[u] << 8);         // bytes lin - 1 .. lin + 2
-            } else {
-                v[u] = on ? load4(mat, lin, n) : 0u;
-                pv[u] = on && diff ? load4(mat, lin - 1, n) : 0u;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint32_t it = base + u * 256 + tid;
-            if (it < items) {
-                const uint32_t r = it / nd, d = it - r * nd;
-                *reinterpret_cast<uint32_t *>(D + r * kDS + 4 * d) = diff ? sub8(v[u], pv[u]) : v[u];
-            }
-        }
-    }
-}
-
 // (row, dword) of the items tid, tid + 256, tid + 512, ... of a tile image nd dwords wide,
 // stepped without a division per item
 struct TileWalk {
@@ -588,11 +543,15 @@ __device__ __forceinline__ TileAt tile_at(const EncArgs &a, const Ws &ws, uint64
     return g;
 }
 
-// The tile image of load_tile in two halves, so that a workgroup can fetch its next tile into
-// registers while it works on the current one: tile_fetch issues the (raw) dword loads, one
-// item per thread and u (the rows' (kTile + 8) / 4 dwords x kTile + 1 rows <= kLU x 256);
-// tile_put stores them and applies the diff model in LDS (each dword's previous byte is the
-// byte before it in the row image; a row's first dword needs only its own byte 2 for byte 3).
+// The LDS image of a tile: rows ty0 - 1 .. ty0 + th - 1, bytes tx0 - 4 .. tx0 + tw - 1 (DT),
+// diff model applied (transform.cpp:220-229: d[k] = m[k] - m[k-1] over the linear matrix,
+// m[-1] = 0). Built in two halves, so that a workgroup fetches its next tile into registers while
+// it works on the current one: tile_fetch issues the raw dword loads (coalesced along each row;
+// one aligned load per dword when the rows are dword-aligned, as in every 512-wide batch), one
+// item per thread and u ((kTile + 8) / 4 dwords x (kTile + 1) rows <= kLU x 256); tile_put
+// stores them and applies the diff model in LDS (each dword's previous byte is the byte before
+// it in the row image; only byte 3 of a row's first dword, x = tx0 - 1, is ever read, and it
+// needs just its own byte 2).
 constexpr uint32_t kLU = ((kTile + 1) * ((kTile + 8) / 4) + 255) / 256;
 __device__ __forceinline__ void tile_fetch(const TileAt &g, uint32_t *v, uint32_t tid)
 {
@@ -635,6 +594,48 @@ __device__ __forceinline__ void tile_put(uint8_t *D, const TileAt &g, uint32_t *
     for (uint32_t u = 0; u < kLU; ++u)
         if (at[u] != ~0u) *reinterpret_cast<uint32_t *>(D + at[u]) = v[u];
     lds_barrier();
+}
+
+// The same image in one go with few registers (emit_tile_kernel, whose occupancy the prefetch
+// registers would halve): 4 items per thread in flight; with dword-aligned rows the diff
+// model's previous byte is the top byte of the dword before, which the lane below loaded
+// (wave_shr 1; lane 0 loads it again).
+__device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64_t n, uint64_t W, uint64_t tx0,
+                                          uint64_t ty0, uint32_t tw, uint32_t th, bool diff, uint32_t tid)
+{
+    const uint32_t nd = (tw + 7) / 4, items = (th + 1) * nd;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(mat) | W) & 3) == 0;
+    const uint32_t lane = tid & 63;
+    constexpr int kU = 4;
+    for (uint32_t base = 0; base < items; base += 256 * kU) {
+        uint32_t v[kU], pv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t it = base + u * 256 + tid;
+            const uint32_t r = it / nd, d = it - r * nd;
+            const int64_t lin = (int64_t)(ty0 + r) * (int64_t)W - (int64_t)W + (int64_t)tx0 - 4 + 4 * (int64_t)d;
+            const bool on = it < items && (r > 0 || ty0 > 0);
+            if (aligned) {
+                const bool whole = on && lin >= 0 && (uint64_t)lin + 4 <= n;
+                v[u] = whole ? *reinterpret_cast<const uint32_t *>(mat + lin) : (on ? load4(mat, lin, n) : 0u);
+                const uint32_t below = lane_shr1(v[u], 0u);
+                const bool own = on && diff && lane == 0 && d > 0;
+                pv[u] = own ? load4(mat, lin - 4, n) : below;  // the dword before (d > 0)
+                pv[u] = (pv[u] >> 24) | (v[u] << 8);         // bytes lin - 1 .. lin + 2
+            } else {
+                v[u] = on ? load4(mat, lin, n) : 0u;
+                pv[u] = on && diff ? load4(mat, lin - 1, n) : 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t it = base + u * 256 + tid;
+            if (it < items) {
+                const uint32_t r = it / nd, d = it - r * nd;
+                *reinterpret_cast<uint32_t *>(D + r * kDS + 4 * d) = diff ? sub8(v[u], pv[u]) : v[u];
+            }
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_cost_kernel(EncArgs a, Ws ws)
@@ -1007,12 +1008,15 @@ __device__ __forceinline__ void emit_block(Value value, uint32_t L, uint8_t *out
     const uint64_t lt = lanes_below(lane);
     uint32_t pv = 0, po = 0;  // value and run offset of the previous step's last element
     uint64_t q = 0;           // bytes written
+    // each step's elements are read one step ahead (lanes past the block read its last element)
+    uint32_t v = value(lane < L ? lane : L - 1);
     for (uint32_t base = 0; base < L; base += 64) {
         const uint32_t p = base + lane;
         const bool valid = p < L;
-        const uint32_t v = valid ? value(p) : 0u;
+        const uint32_t pn = p + 64;
+        const uint32_t vn = value(pn < L ? pn : L - 1);
         const uint32_t prev = lane_shr1(v, pv);
-        const uint32_t nx = dpp<0x130>(v, base + 64 < L ? value(base + 64) : 0u);  // wave_shl 1
+        const uint32_t nx = dpp<0x130>(v, readlane(vn, 0));  // wave_shl 1: the next element
         const bool start = p == 0 || v != prev;
         const uint64_t sm = ballot(valid && start);
         const uint64_t le = sm & (lt | (1ull << lane));
@@ -1030,6 +1034,7 @@ __device__ __forceinline__ void emit_block(Value value, uint32_t L, uint8_t *out
         q += __popcll(b1) + __popcll(b2);
         po = readlane(o, 63);
         pv = readlane(v, 63);
+        v = vn;
     }
 }
 
@@ -1040,36 +1045,51 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
     __shared__ uint8_t D[(kTile + 1) * kDS];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[0];
+    const bool diff = a.diff != 0;
+    // (no prefetch of the next tile as in tile_cost_kernel: its registers across the emit loop
+    // cost half the occupancy, measured slower)
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t i = find_item(ws.idx[0], a.n, t, ws.ctr[8 + 0]);
-        const AMeta &M = ws.meta[i];
-        if (M.status || M.B > kTile) continue;  // (uniform over the workgroup)
-        const uint64_t W = M.w, H = M.h, B = M.B;
-        const uint64_t ntx = cdiv(W, kTile), local = t - ws.idx[0][i];
-        const uint64_t tx0 = (local % ntx) * kTile, ty0 = (local / ntx) * kTile;
-        const uint32_t tw = (uint32_t)(W - tx0 < kTile ? W - tx0 : kTile);
-        const uint32_t th = (uint32_t)(H - ty0 < kTile ? H - ty0 : kTile);
-        load_tile(D, a.in + a.in_offs[i], W * H, W, tx0, ty0, tw, th, a.diff != 0, tid);
+        const TileAt g = tile_at(a, ws, t);
+        if (!g.ok || ws.meta[g.i].B > kTile) continue;  // (uniform over the workgroup)
+        load_tile(D, g.mat, g.n, g.W, g.tx0, g.ty0, g.tw, g.th, diff, tid);
         lds_barrier();
+        const uint32_t i = g.i;
+        const AMeta &M = ws.meta[i];
+        const uint64_t W = g.W, B = M.B, tx0 = g.tx0, ty0 = g.ty0;
+        const uint32_t tw = g.tw, th = g.th;
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
         const uint32_t *offw = at<uint32_t>(ws, M.cost0[M.best]);
         const uint32_t b32 = (uint32_t)B;
         const uint32_t nbx = (tw + b32 - 1) / b32, nby = (th + b32 - 1) / b32;
         const uint64_t per_row = cdiv(W, B);
-        for (uint32_t b = wv; b < nbx * nby; b += 4) {
+        // the wave's blocks b = wv + 4 m: each lane fetches one block's offset and scan order
+        // (64 blocks per fetch), so no block waits on a global load of its own
+        const uint32_t nblk = nbx * nby;
+        uint32_t lane_off = 0, lane_h = 0;
+        for (uint32_t b = wv; b < nblk; b += 4) {
+            const uint32_t m = ((b - wv) >> 2) & 63;
+            if (m == 0) {
+                const uint32_t bl = b + 4 * lane;
+                if (bl < nblk) {
+                    const uint64_t kl = (ty0 / B + bl / nbx) * per_row + tx0 / B + bl % nbx;
+                    lane_off = offw[kl];
+                    lane_h = (sym[24 + kl / 8] >> (7 - kl % 8)) & 1;
+                }
+            }
             const uint32_t bx = b % nbx, by = b / nbx;
             const uint32_t x0 = bx * b32, y0 = by * b32;
             const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
-            const uint64_t k = (ty0 / B + by) * per_row + tx0 / B + bx;
-            const bool horiz = (sym[24 + k / 8] >> (7 - k % 8)) & 1;
+            const bool horiz = readlane(lane_h, m) != 0;
             const uint32_t inner = horiz ? sx : sy;
             const float inv = 1.0f / (float)inner;
+            const bool pow2 = (inner & (inner - 1)) == 0;  // whole blocks: shifts, not a division
+            const uint32_t lgi = (uint32_t)__builtin_ctz(inner);
             auto value = [&](uint32_t p) -> uint32_t {
-                const uint32_t a1 = div_small(p, inner, inv), b1 = p - a1 * inner;
+                const uint32_t a1 = pow2 ? p >> lgi : div_small(p, inner, inv), b1 = p - a1 * inner;
                 const uint32_t xl = x0 + (horiz ? b1 : a1), yl = y0 + (horiz ? a1 : b1);
                 return DT(yl + 1, xl);
             };
-            emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + offw[k], lane);
+            emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + readlane(lane_off, m), lane);
         }
         lds_barrier();
     }
@@ -1561,11 +1581,13 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
             const uint64_t gby = ty0 / B + by;
             uint64_t pos = starts[gby * ntx + tix];
             rd.start(pos);
+            // the row's scan orders, one block per lane (nbx <= 16)
+            const uint64_t kl = gby * per_row + tx0 / B + lane;
+            const uint32_t lane_h = lane < nbx ? (sym[24 + kl / 8] >> (7 - kl % 8)) & 1 : 0u;
             for (uint32_t bx = 0; bx < nbx; ++bx) {
-                const uint64_t k = gby * per_row + tx0 / B + bx;
                 const uint32_t x0 = bx * b32, y0 = by * b32;
                 const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
-                const bool horiz = (sym[24 + k / 8] >> (7 - k % 8)) & 1;
+                const bool horiz = readlane(lane_h, bx) != 0;
                 const uint32_t inner = horiz ? sx : sy;
                 const float inv = 1.0f / (float)inner;
                 auto place = [&](uint64_t q, uint32_t v) {
