@@ -73,6 +73,7 @@ struct AMeta {
     unsigned long long total[kCand];  // encode: data bytes of candidate c
     uint64_t nbc[kCand];             // encode: blocks of candidate c
     uint64_t pieces;                 // encode: first tile-summary entry
+    uint64_t offs;                   // encode: the winner's u64 block offsets (workspace offset)
     uint64_t slab;                   // first byte of the stream's workspace slab
     uint64_t sym;                    // first symbol byte (workspace offset)
     uint64_t starts;                 // decode: first group-start entry (workspace offset, bytes)
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(1024) void enc_plan_kernel(EncArgs a, Ws ws)
         v[0] = ok ? ntx * nty : 0;
         v[1] = big;
         v[2] = nb8;
-        v[3] = ok ? align_up(4 * cost, 16) + align_up(8 * pieces, 16) + align_up(syms, 16) : 0;
+        v[3] = ok ? align_up(4 * cost, 16) + align_up(8 * pieces, 16) + align_up(8 * nb8, 16) + align_up(syms, 16) : 0;
     };
     auto put = [&](uint32_t i, const uint64_t *base) {
         uint64_t v[4];
@@ -435,6 +436,8 @@ __global__ __launch_bounds__(1024) void enc_plan_kernel(EncArgs a, Ws ws)
         o = align_up(o, 16);
         m.pieces = o;
         o += align_up(v[3] ? 8 * (nc > kTileCand ? h * cdiv(w, kTile) + w * cdiv(h, kTile) : 0) : 0, 16);
+        m.offs = o;  // one u64 per block of the winner (at most the B = 8 count)
+        o += align_up(v[3] ? 8 * v[2] : 0, 16);
         m.sym = o;
         ws.sym_offs[i] = o;
         ws.sym_lens[i] = 0;
@@ -954,7 +957,7 @@ __global__ __launch_bounds__(256) void choose_kernel(EncArgs a, Ws ws)
             sym[24 + k] = (uint8_t)byte;
         }
         __syncthreads();
-        // exclusive scan of the chosen lengths, written over the words (u32: < 2^32 data bytes)
+        // exclusive scan of the chosen lengths into the u64 block offsets
         const uint64_t per = (nb + 255) / 256, lb = tid * per, le = lb + per < nb ? lb + per : nb;
         uint64_t s = 0;
         for (uint64_t k = lb; k < le; ++k) s += wd[k] & 0x7FFFFFFFu;
@@ -970,10 +973,10 @@ __global__ __launch_bounds__(256) void choose_kernel(EncArgs a, Ws ws)
         }
         __syncthreads();
         s = part[tid];
+        uint64_t *offs = at<uint64_t>(ws, M.offs);
         for (uint64_t k = lb; k < le; ++k) {
-            const uint32_t v = wd[k] & 0x7FFFFFFFu;
-            wd[k] = (uint32_t)s;
-            s += v;
+            offs[k] = s;
+            s += wd[k] & 0x7FFFFFFFu;
         }
         if (tid == 0) {
             M.nb = nb;
@@ -981,7 +984,6 @@ __global__ __launch_bounds__(256) void choose_kernel(EncArgs a, Ws ws)
             M.best = best;
             M.hdr = hdr;
             M.count = best_len;
-            if (M.total[best] >= 0xFFFFFFFFull) M.status = HC_ERR_UNSUPPORTED;
             ws.sym_lens[i] = M.status ? 0 : best_len;
         }
         __syncthreads();
@@ -1058,14 +1060,15 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
         const uint64_t W = g.W, B = M.B, tx0 = g.tx0, ty0 = g.ty0;
         const uint32_t tw = g.tw, th = g.th;
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
-        const uint32_t *offw = at<uint32_t>(ws, M.cost0[M.best]);
+        const uint64_t *offw = at<uint64_t>(ws, M.offs);
         const uint32_t b32 = (uint32_t)B;
         const uint32_t nbx = (tw + b32 - 1) / b32, nby = (th + b32 - 1) / b32;
         const uint64_t per_row = cdiv(W, B);
         // the wave's blocks b = wv + 4 m: each lane fetches one block's offset and scan order
         // (64 blocks per fetch), so no block waits on a global load of its own
         const uint32_t nblk = nbx * nby;
-        uint32_t lane_off = 0, lane_h = 0;
+        uint64_t lane_off = 0;
+        uint32_t lane_h = 0;
         for (uint32_t b = wv; b < nblk; b += 4) {
             const uint32_t m = ((b - wv) >> 2) & 63;
             if (m == 0) {
@@ -1089,7 +1092,8 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
                 const uint32_t xl = x0 + (horiz ? b1 : a1), yl = y0 + (horiz ? a1 : b1);
                 return DT(yl + 1, xl);
             };
-            emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + readlane(lane_off, m), lane);
+            const uint64_t off = readlane((uint32_t)lane_off, m) | (uint64_t)readlane((uint32_t)(lane_off >> 32), m) << 32;
+            emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + off, lane);
         }
         lds_barrier();
     }
@@ -1126,7 +1130,7 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EncArgs a, Ws ws)
             if (diff) v = (v - (lin ? mat[lin - 1] : 0u)) & 0xFFu;
             return v;
         };
-        emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + at<uint32_t>(ws, M.cost0[M.best])[k], lane);
+        emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + at<uint64_t>(ws, M.offs)[k], lane);
     }
 }
 
@@ -1152,9 +1156,10 @@ struct DecArgs {
     int32_t *status;
 };
 
-// u32 block-start entries per stream: mode 0 ceil(H/B) * ceil(W/128) <= cap/8 + cap/128 +
-// cap/1024 + 1; mode 1 far fewer; mode 2 <= 4 W H / 1024 + 1 (dec_header_kernel)
-__device__ __forceinline__ uint64_t group_entries_bound(uint64_t cap) { return cap / 7 + 16; }
+// u64 block-start entries per stream (W H <= cap, W, H >= 8): mode 0 ceil(H/B) ceil(W/128) <=
+// (H/8 + 1)(W/128 + 1) <= WH/1024 + WH/64 + WH/1024 + 1; mode 1 far fewer; mode 2
+// <= 4 W H / 1024 + 1 (dec_header_kernel)
+__device__ __forceinline__ uint64_t group_entries_bound(uint64_t cap) { return cap / 32 + 16; }
 
 // symbols the FGK stage may write: the count, unless the payload cannot hold it (the first symbol
 // takes >= 8 bits, every later one >= 1), which the FGK decoder reports as 9 without writing
@@ -1175,7 +1180,7 @@ __global__ __launch_bounds__(1024) void dec_plan_kernel(DecArgs a, Ws ws)
             for (int b = 7; b >= 0; --b) count = count << 8 | p[b];
         const bool ok = len >= 9 && (p[8] & HC_FLAG_ADAPT);
         const uint64_t oc = a.out_caps[i];
-        v[0] = ok ? align_up(sym_cap(count, len) + 64, 16) + align_up(4 * group_entries_bound(oc) + oc / kChunk + 16, 16)
+        v[0] = ok ? align_up(sym_cap(count, len) + 64, 16) + align_up(8 * group_entries_bound(oc) + oc / kChunk + 16, 16)
                   : 0;
     };
     auto put = [&](uint32_t i, const uint64_t *base) {
@@ -1194,7 +1199,7 @@ __global__ __launch_bounds__(1024) void dec_plan_kernel(DecArgs a, Ws ws)
             for (int b = 7; b >= 0; --b) count = count << 8 | p[b];
         const uint64_t cap = m.status ? 0 : sym_cap(count, len);
         m.starts = m.slab + align_up(cap + 64, 16);
-        m.csum = m.starts + 4 * group_entries_bound(a.out_caps[i]);
+        m.csum = m.starts + 8 * group_entries_bound(a.out_caps[i]);
         ws.sym_offs[i] = m.sym;
         ws.sym_caps[i] = cap;
         ws.sym_lens[i] = 0;
@@ -1340,7 +1345,7 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
         AMeta &M = ws.meta[i];
         if (M.status) continue;
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
-        uint32_t *starts = at<uint32_t>(ws, M.starts);
+        uint64_t *starts = at<uint64_t>(ws, M.starts);
         const uint64_t per_row = cdiv(M.w, M.B), ntx = cdiv(M.w, kTile);
         // the entry of block k (or ~0 if k starts no group)
         auto entry = [&](uint64_t k) -> uint64_t {
@@ -1363,7 +1368,7 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
         uint64_t blk = 0, got = 0;
         uint32_t r = 0, last = 0;
         int status = 0;
-        if (lane == 0 && nb) starts[0] = (uint32_t)pos;
+        if (lane == 0 && nb) starts[0] = pos;
         uint64_t want = 0;
         if (nb) {
             uint64_t x0, y0, sx, sy;
@@ -1445,7 +1450,7 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
                 ++blk;
                 if (blk < nb && lane == 0) {
                     const uint64_t e = entry(blk);
-                    if (e != ~0ull) starts[e] = (uint32_t)(pos + lo);
+                    if (e != ~0ull) starts[e] = pos + lo;
                 }
                 if (blk == nb) {
                     pos += lo;
@@ -1570,7 +1575,7 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
         const uint32_t b32 = (uint32_t)B;
         const uint32_t nbx = (tw + b32 - 1) / b32, nby = (th + b32 - 1) / b32;
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
-        const uint32_t *starts = at<uint32_t>(ws, M.starts);
+        const uint64_t *starts = at<uint64_t>(ws, M.starts);
         const uint64_t per_row = cdiv(W, B);
         SymRing rd;
         rd.R = reinterpret_cast<uint8_t *>(ring[wv]);
@@ -1626,7 +1631,7 @@ __global__ __launch_bounds__(256) void unblock_kernel(DecArgs a, Ws ws)
         if (M.status || M.mode == 0) continue;
         const uint64_t g = t - ws.idx[0][i];
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
-        uint64_t pos = at<uint32_t>(ws, M.starts)[g];
+        uint64_t pos = at<uint64_t>(ws, M.starts)[g];
         uint8_t *mat = a.out + a.out_offs[i];
         const uint64_t W = M.w;
         const uint64_t kb = g * M.K, ke = kb + M.K < M.nb ? kb + M.K : M.nb;
@@ -1768,15 +1773,16 @@ unsigned resident_grid(Kernel k, unsigned threads)
 
 uint64_t adapt_encode_work_bound(uint64_t total_in, uint32_t n)
 {
-    // per matrix of L bytes: cost words <= L/3, tile summaries <= 0.19 L, symbols <= 1.41 L + 42
-    return ws_header(n) + 2 * total_in + 128ull * n + 4096;
+    // per matrix of L bytes: cost words <= L/3, tile summaries <= 0.19 L, u64 block offsets
+    // <= 8 (3L/64 + 1), symbols <= 1.41 L + 42
+    return ws_header(n) + 5 * (total_in / 2) + 5 + 176ull * n + 4096;
 }
 
 uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t n)
 {
-    // symbols <= 8 per payload byte (+64 slack); u32 block starts <= out_cap / 7 + 16 (see
+    // symbols <= 8 per payload byte (+64 slack); u64 block starts <= 8 (out_cap / 32 + 16) (see
     // group_entries_bound); chunk sums out_cap / 16384
-    return ws_header(n) + 8 * total_in + total_out / 7 * 4 + total_out / kChunk + 192ull * n + 4096;
+    return ws_header(n) + 8 * total_in + total_out / 4 + total_out / kChunk + 320ull * n + 4096;
 }
 
 hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work, uint64_t work_bytes,

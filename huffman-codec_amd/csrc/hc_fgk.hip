@@ -49,6 +49,10 @@ __device__ uint32_t g_window = 1u << 30;
 // launchers pass it in Batch::min_tree.
 static uint32_t g_min_tree = 0;
 
+// Encoder mode for narrow / wide streams: 0 = per stream by enc_mode_kernel (default), 1 = path
+// cache for all, 2 = tables for all (hc_debug_set_enc_tab; tests run both on every input)
+static uint32_t g_enc_tab = 0;
+
 // the tree layout for a stream of at most `max_sym` FGK symbols
 __device__ __forceinline__ uint32_t tree_kind(uint64_t max_sym, uint32_t lo)
 {
@@ -154,8 +158,9 @@ using WeightT = std::conditional_t<kW == 2, uint64_t, uint32_t>;
 
 // One wavefront's LDS; <= 5 KB so that 8 four-wave workgroups fit a CU (narrow). Encoder and
 // decoder each add their cache (tests/fgk_cache_model.py is the executable model of both,
-// checked against the plain slot form).
-template <int kW, bool kDec>
+// checked against the plain slot form). kTab: the encoder's table mode (no path cache; the
+// decoder's level tables plus pcode[], ~6.5 KB, 6 waves per SIMD).
+template <int kW, bool kDec, bool kTab = false>
 struct alignas(16) Tree {
     WeightT<kW> wt[kWords];           // narrow: weight << 10 | parent; wide / huge: weight
     uint32_t scratch[kW == 2 ? 128 : 64];  // landing words of lanes that must not write
@@ -170,14 +175,17 @@ struct alignas(16) Tree {
     // address reads a lane's position and (lane 0) the row's metadata.
     // row "entry -1" (where[] entry 0: not cached): level 0 at sentinel position kMissPos, whose
     // leader test always fails at lane 0, so a miss leaves the hot loop like a failed update
-    alignas(16) uint16_t pc_miss[kDec ? 2 : kRow];
-    uint16_t pc[kDec ? 2 : kSlots * kRow];
+    alignas(16) uint16_t pc_miss[(kDec || kTab) ? 2 : kRow];
+    uint16_t pc[(kDec || kTab) ? 2 : kSlots * kRow];
     alignas(8) uint32_t syms[kDec ? 64 : kSymWords];  // MNP-5 symbols: encoder one chunk, decoder one block
     // decoder level tables: level j (1..8) at 2^j - 2 + prefix: position | depth << 10 where
     // the walk from the root along the prefix's bits stops; lvl_root (indices -2, -1: "level
     // 0") holds the root, which the lanes above a path's depth read
     uint16_t lvl_root[2];
-    uint16_t lvl[kDec ? 512 : 2];
+    uint16_t lvl[(kDec || kTab) ? 512 : 2];
+    // table mode: position -> its code as the level tables reached it: the prefix left-aligned
+    // to 8 bits | (depth - 1) << 8 (checked against the tables at every use: stale entries fail)
+    uint16_t pcode[kTab ? 516 : 2];
 };
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -276,14 +284,15 @@ __device__ __forceinline__ void buf_store8(rsrc_t r, uint32_t off, uint32_t v)
 
 // ------------------------------------------------------------------------------ the tree --
 
-template <int kW, bool kDec>
+template <int kW, bool kDec, bool kTab = false>
 struct Fgk {
+    static constexpr bool kTabs = kDec || kTab;  // keeps the level tables
     static constexpr bool kWide = kW != 0;  // weights apart from parents (wide / huge)
     static constexpr bool kHuge = kW == 2;  // 64-bit weights
     using Wt = WeightT<kW>;
     static constexpr Wt kInc = kWide ? 1u : 1024u;
 
-    Tree<kW, kDec> &T;
+    Tree<kW, kDec, kTab> &T;
     uint32_t lane;
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
@@ -298,15 +307,15 @@ struct Fgk {
     const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
     uint64_t pacc = 0;        // HC_PROF regions inside the tree code
 
-    __device__ Fgk(Tree<kW, kDec> &t, uint32_t l)
+    __device__ Fgk(Tree<kW, kDec, kTab> &t, uint32_t l)
         : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), pc_lb(0), pc_lb_ok(0), gen(0), stale(0), from(0),
-          pc_lane(&t.pc[0] + (l & 15u) - (kDec ? 0 : kRow))
+          pc_lane(&t.pc[0] + (l & 15u) - (kTabs ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
         // narrow: sentinels above every weight word; the encoder's last word (above kMissPos)
         // is 0 and the decoder's are all ones - 1, see update_fast
         for (uint32_t i = lane; i < kWords; i += 64)
-            T.wt[i] = i <= kRoot ? (Wt)0 : (kWide ? ~(Wt)0 : (Wt)(kDec ? 0xFFFFFFFEu : (i != kWords - 1 ? 0xFFFFFFFFu : 0u)));
+            T.wt[i] = i <= kRoot ? (Wt)0 : (kWide ? ~(Wt)0 : (Wt)(kTabs ? 0xFFFFFFFEu : (i != kWords - 1 ? 0xFFFFFFFFu : 0u)));
         if (lane < 2) T.lvl_root[lane] = kRoot;
         for (uint32_t i = lane; i < 516; i += 64) {
             T.body[i] = i == kRoot ? (kDec ? kNyt | kNotLeaf : kNyt) : 0;
@@ -314,8 +323,12 @@ struct Fgk {
         }
         if (!kDec) {
             for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
-            for (uint32_t i = lane; i < kSlots * kRow; i += 64) T.pc[i] = (i % kRow) < kSlotDepth ? 0xFFFF : 0;
-            if (lane < kRow) T.pc_miss[lane] = lane == 0 ? kMissPos : kRoot;
+            if constexpr (kTab) {
+                for (uint32_t i = lane; i < 516; i += 64) T.pcode[i] = 0;
+            } else {
+                for (uint32_t i = lane; i < kSlots * kRow; i += 64) T.pc[i] = (i % kRow) < kSlotDepth ? 0xFFFF : 0;
+                if (lane < kRow) T.pc_miss[lane] = lane == 0 ? kMissPos : kRoot;
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -466,6 +479,8 @@ struct Fgk {
                 *(on && inner ? &T.body[x] : scr16()) = (uint16_t)((b & kContent) | (gen << kMarkShift));
                 const uint32_t ne = inner ? (((b & 255u) * 2 + (q & 1u)) | (j << 10)) : pe;
                 *(on ? &T.lvl[cnt - 2 + q] : scr16()) = (uint16_t)ne;
+                if constexpr (kTab)  // the child reached at depth j has code q
+                    *(on && inner ? &T.pcode[(b & 255u) * 2 + (q & 1u)] : scr16()) = (uint16_t)((q << (8 - j)) | ((j - 1) << 8));
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -511,7 +526,7 @@ struct Fgk {
     {
         // encoder: drop the cached paths through s or l first (scan: they may lie on one); the
         // relink below then gives a moved leaf's where[] its new position
-        if (!kDec && scan) {
+        if (!kTabs && scan) {
             HC_PROF_BEGIN();
             pc_swapped(s, l);
             HC_PROF_END(7);
@@ -520,12 +535,13 @@ struct Fgk {
         // moving to l; lanes 2, 3 (lane >> 1 = 1) re-parent the second child of the same content
         const uint32_t pos = (lane & 1) ? l : s;        // where the lane's content goes
         const uint32_t b = T.body[(lane & 1) ? s : l];  // that content
-        if (kDec) {
+        if (kTabs) {
             // generation marks stay with the positions: the destination's own word is the
             // partner lane's read (quad_perm [1,0,3,2])
             const uint32_t bo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & kContent) | (bo & (31u << kMarkShift)));
             if (ballot(lane < 2 && ((b >> kMarkShift) & 31u) == gen)) from = min(from, table_level(s, l) + 1);
+            if (!kDec) *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
         } else {
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;
             *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
@@ -581,7 +597,7 @@ struct Fgk {
         int32_t km = -64;       // levels - 64
         uint32_t s = vreg(s0);  // per-level work on the VALU (see vreg)
         uint32_t td = kRoot;    // lane j: level k - 1 - j
-        if (!kDec) {
+        if (!kTabs) {
             // encoder: kProbe levels, then look the position up in the path cache: a cached
             // path through it (rows stay valid paths) gives the rest of the climb at once
 #pragma unroll
@@ -620,7 +636,7 @@ struct Fgk {
                 }
             }
         }
-        if (kDec || uni(s) != kRoot) do {
+        if (kTabs || uni(s) != kRoot) do {
             // wave_shr:1, lane 0 taking s
             const uint32_t sh = __builtin_amdgcn_update_dpp(0u, td, 0x138, 0xF, 0xF, true);
             td = lane == 0 ? s : sh;
@@ -948,13 +964,88 @@ struct RecSink {
 // Waves per SIMD each tree layout's LDS admits (8 four-wave workgroups per CU narrow, 6 wide, 4
 // huge): the register budget the compiler may use (fewer scalar spills in the wide kernels,
 // which C4's single long stream runs)
-template <int kW>
-constexpr int kWavesPerSimd = kW == 0 ? 8 : (kW == 1 ? 6 : 4);
+template <int kW, bool kTab = false>
+constexpr int kWavesPerSimd = kTab ? (kW == 0 ? 6 : 5) : (kW == 0 ? 8 : (kW == 1 ? 6 : 4));
 
-template <int kW, int kSrc>
-__global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW>))) void encode_kernel(Batch bt)
+// Which way the encoder finds codes, voted per stream (status[] carries the vote, then the batch's
+// choice, until the encoder overwrites it with the stream's status): the path cache when the
+// stream's 16 most frequent
+// symbols cover most of it (>= 60 %: the diff model's photos, 96 %), the level tables when the
+// alphabet is flat (< 15 %: noise, ramps, 6-8 %) -- measured: photo -c -m 8192 streams cache 67
+// ms / tables 131, noise -c -m 2048 485 / 227, ramps -c 8192 623 / 365 -- and in between (photos
+// without the diff model, ~25 %) the tables only when every stream is resident at once in table
+// mode's occupancy (photo -c 4096 streams 325 / 231 ms, 8192 401 / 436; the 4096^2 -c -a
+// matrix, one stream, 6.25 / 2.97 s). Estimated from the first 16 KB: the byte of every run
+// start (diff model applied), a 256-bin histogram per wave in LDS, the top 16 by repeated max.
+constexpr int32_t kModeTables = -0x7A0, kModeCache = -0x7A1;
+template <int kSrc>
+__global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_occ, uint32_t forced)
 {
-    __shared__ Tree<kW, false> trees[kWaves];
+    __shared__ uint32_t hist[4][256];
+    const uint32_t lane = lane_id(), wv = uni(threadIdx.x >> 6);
+    const uint32_t sid = blockIdx.x * 4 + wv;
+    if (sid >= bt.n) return;
+    if (forced) {
+        if (lane == 0) bt.status[sid] = forced == 2 ? kModeTables : kModeCache;
+        return;
+    }
+    uint32_t *h = hist[wv];
+    for (uint32_t i = lane; i < 256; i += 64) h[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t *in = bt.in + bt.in_offs[sid];
+    const uint64_t n = bt.in_lens[sid];
+    const uint32_t m = (uint32_t)min(n, (uint64_t)16384);
+    uint32_t prev = 0, total = 0;  // the byte before this lane's, run starts
+    for (uint32_t b = 0; b < m; b += 64) {
+        const uint32_t i = b + lane;
+        uint32_t v = i < m ? in[i] : 0u;
+        if (kSrc == SRC_RAW_DIFF) v = (v - (i ? (i - 1 < m ? in[i - 1] : 0u) : 0u)) & 255u;
+        const uint32_t up = __shfl_up(v, 1, 64);
+        const uint32_t pv = lane == 0 ? prev : up;
+        const bool start = i < m && (i == 0 || v != pv);
+        if (start) atomicAdd(&h[v], 1u);
+        total += (uint32_t)__builtin_popcountll(ballot(start));
+        prev = lane_read(v, 63);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t c[4], top = 0;
+    for (uint32_t k = 0; k < 4; ++k) c[k] = h[64 * k + lane];
+    for (uint32_t r = 0; r < 16; ++r) {
+        uint32_t mx = max(max(c[0], c[1]), max(c[2], c[3]));
+        for (uint32_t d = 32; d; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+        top += mx;
+        const uint64_t who = ballot(c[0] == mx || c[1] == mx || c[2] == mx || c[3] == mx);
+        if (lane == (uint32_t)__builtin_ctzll(who)) {  // take out one of the maxima
+            if (c[0] == mx) c[0] = 0;
+            else if (c[1] == mx) c[1] = 0;
+            else if (c[2] == mx) c[2] = 0;
+            else c[3] = 0;
+        }
+    }
+    const bool cache = total == 0 || 100ull * top >= 60ull * total || (100ull * top >= 15ull * total && !low_occ);
+    if (lane == 0) bt.status[sid] = cache ? kModeCache : kModeTables;
+}
+
+// The batch follows its majority: split between the cache and the table launches (which run one
+// after the other) each would hold only part of the GPU (measured: photo -c 8192 streams 600 ms
+// split by stream, against 402 / 427 ms in one mode)
+__global__ __launch_bounds__(1024) void enc_mode_vote_kernel(Batch bt)
+{
+    __shared__ uint32_t votes;
+    if (threadIdx.x == 0) votes = 0;
+    __syncthreads();
+    uint32_t v = 0;
+    for (uint32_t i = threadIdx.x; i < bt.n; i += 1024) v += bt.status[i] == kModeTables;
+    atomicAdd(&votes, v);
+    __syncthreads();
+    const int32_t mode = 2ull * votes > bt.n ? kModeTables : kModeCache;
+    for (uint32_t i = threadIdx.x; i < bt.n; i += 1024) bt.status[i] = mode;
+}
+
+template <int kW, int kSrc, bool kTab = false>
+__global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW, kTab>))) void encode_kernel(Batch bt)
+{
+    __shared__ Tree<kW, false, kTab> trees[kWaves];
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
@@ -972,9 +1063,11 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // other layouts' launches skip the stream
     const uint64_t max_sym = kSrc == SRC_SYMBOLS ? n : n + n / 3 + 2;
     if (tree_kind(max_sym, bt.min_tree) != (uint32_t)kW) return;
+    // narrow and wide: the cache and the table launches split the streams (enc_mode_kernel)
+    if (kW <= 1 && (uni(bt.status[sid]) == kModeTables) != kTab) return;
     const uint32_t window = uni(g_window);
 
-    Fgk<kW, false> fgk(trees[wv], lane);
+    Fgk<kW, false, kTab> fgk(trees[wv], lane);
     RecSink sink;
     sink.rs = make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
     sink.wbase = 0;
@@ -1106,6 +1199,99 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         }
     };
 
+    // Table mode (kTab): no path cache. The decoder's level tables (levels 1..8, prefix ->
+    // where the walk from the root stops) and pcode[] (position -> the code the tables reached
+    // it by) give a symbol's code and whole root path from three reads: where[] -> pcode[] ->
+    // one lane-parallel read of the tables (lane k: level 8 - k), exactly the decoder's path
+    // read. The level-8 entry read back must name the symbol's own position at the pcode depth;
+    // otherwise (deeper than 8, or not in the tables since a split) the symbol is coded from
+    // scratch like a cache miss. A symbol's reads go out up to three symbols ahead (where[],
+    // pcode[] and the tables change only on the paths that leave the loop).
+    const uint32_t psh = lane < 8 ? lane : 8u;
+    const uint32_t pbase = lds_off16(&fgk.T.lvl[0]) + 2 * (lane < 8 ? (256u >> lane) - 2 : 0xFFFFFFFEu);
+    auto path_read = [&](uint32_t pcw) __attribute__((always_inline)) {
+        return opaque(*(const lds_u16 *)(size_t)(pbase + ((pcw & 255u) >> psh) * 2));
+    };
+    auto miss_tab = [&](uint32_t sv) {
+        const uint32_t sym = uni(sv);
+        uint32_t s = uni(fgk.T.where[sym]) & 1023u;
+        const uint32_t fresh = s == 0;
+        if (fresh) s = uni(fgk.split(sym));
+        uint32_t pv;
+        const uint32_t d = fgk.chase(s, pv);
+        const uint64_t bits = ballot(pv & 1u);
+        if (!fresh && d <= 8) {  // the tables are short of it (a split since the last build)
+            if (++fgk.stale >= kRefresh) fgk.from = 0;
+        }
+        if (d > kInsertDepth) fgk.walk(s, pv);
+        else fgk.update_path(pv);
+        if (fresh) {
+            sink.push_bits(bits >> 1, d - 1);
+            sink.push((1u << 8) | sym);
+        } else {
+            sink.push_bits(bits, d);
+        }
+    };
+    auto code_all_tab = [&](uint32_t ns) __attribute__((always_inline)) {
+        uint32_t t = 0;
+        while (t < ns) {
+            if (fgk.from < 9) fgk.build_levels();
+            uint32_t rl = sink.n;
+            const uint32_t rend = min(64u, rl + (ns - t));
+            const uint32_t x1 = vreg(fgk.T.where[sb[t + 1]]);
+            const uint32_t x0 = vreg(fgk.T.where[sb[t]]);
+            uint32_t pc0 = vreg(fgk.T.pcode[x0 & 1023u]);   // pcode of t
+            uint32_t pr = path_read(pc0);                      // path of t
+            uint32_t x0u = x0;
+            uint32_t pc1 = vreg(fgk.T.pcode[x1 & 1023u]);   // pcode of t+1
+            uint32_t x1u = x1;
+            uint32_t x2 = vreg(fgk.T.where[sb[t + 2]]);      // where[] of t+2
+            uint32_t sv3 = vreg(sb[t + 3]);                    // byte of t+3
+            const lds_u8 *vb = (const lds_u8 *)sb + t + 4;
+            asm("" : "+v"(vb));
+            uint32_t pv, k, ok;
+            int32_t left = (int32_t)(rl - rend);
+            do {
+                const uint32_t pcu = uni(pc0);
+                const uint32_t d = ((pcu >> 8) & 7u) + 1;
+                ok = uni(pr) == ((uni(x0u) & 1023u) | (d << 10));
+                const uint32_t rec = (1u << d) | ((pcu & 255u) >> (8 - d));
+                pv = pr & 1023u;
+                uint32_t prn;
+                k = fgk.update_fast(pv, [&] {
+                    prn = path_read(pc1);
+                    const uint32_t pc2 = fgk.T.pcode[x2 & 1023u];
+                    const uint32_t x3 = fgk.T.where[sv3];
+                    const uint32_t sv4 = *vb;
+                    x0u = x1u;
+                    x1u = x2;
+                    pc0 = pc1;
+                    pc1 = pc2;
+                    x2 = x3;
+                    sv3 = sv4;
+                }, ok ? 0u : 0xFFFFFFFFu);
+                pr = prn;
+                sink.vrec = writelane(sink.vrec, rec, (uint32_t)((int32_t)rend + left));
+                ++vb;
+                ++left;
+            } while ((int32_t)(k & (uint32_t)left) < 0);
+            rl = (uint32_t)((int32_t)rend + left);
+            t += rl - sink.n;
+            if (k != 0xFFFFFFFFu) {
+                if (!ok) {  // not in the tables: nothing was stored; code it from scratch
+                    --t;
+                    sink.n = rl - 1;  // its record lane, overwritten by the miss path
+                    miss_tab(sb[t]);
+                    ++t;
+                    continue;
+                }
+                fgk.walk(lane_read(pv, k), pv);
+            }
+            sink.n = rl;
+            if (rl == 64) sink.pack();
+        }
+    };
+
     uint64_t nsym = 0;
     uint32_t next = buf_load(rin, lane * 4);
     RleCarry cy = {0, 0, 0};
@@ -1130,7 +1316,8 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
                 fgk.T.syms[lane] = chunk;
                 __builtin_amdgcn_wave_barrier();
-                code_all(m);
+                if constexpr (kTab) code_all_tab(m);
+                else code_all(m);
                 nsym += m;
                 continue;
             }
@@ -1139,7 +1326,8 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             const uint32_t ns = rle_chunk<kSrc>(chunk, m, ci + 1 == nch ? 1u : 0u, cy, fgk.T.syms,
                                                 fgk.scr32(), lane);
             HC_PROF_END(4);
-            code_all(ns);
+            if constexpr (kTab) code_all_tab(ns);
+            else code_all(ns);
             nsym += ns;
         }
     };
@@ -1556,29 +1744,43 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
 
 }  // namespace
 
+// streams that the table-mode encoder holds resident at once: 6 waves per SIMD (its LDS)
+static uint32_t table_slots()
+{
+    static uint32_t slots = 0;
+    if (!slots) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        slots = (uint32_t)cus * 24;
+    }
+    return slots;
+}
+
+template <int kSrc>
+static void launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipStream_t st)
+{
+    enc_mode_kernel<kSrc><<<(b.n + 3) / 4, 256, 0, st>>>(b, b.n <= table_slots() ? 1u : 0u, g_enc_tab);
+    if (!g_enc_tab) enc_mode_vote_kernel<<<1, 1024, 0, st>>>(b);
+    encode_kernel<0, kSrc><<<grid, block, 0, st>>>(b);
+    encode_kernel<0, kSrc, true><<<grid, block, 0, st>>>(b);
+    encode_kernel<1, kSrc><<<grid, block, 0, st>>>(b);
+    encode_kernel<1, kSrc, true><<<grid, block, 0, st>>>(b);
+    encode_kernel<2, kSrc><<<grid, block, 0, st>>>(b);
+}
+
 hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st)
 {
     if (b0.n == 0) return hipSuccess;
     Batch b = b0;
     b.min_tree = g_min_tree;
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
-    // one launch per tree layout; each stream is coded by exactly one of them (tree_kind)
+    // enc_mode_kernel marks each stream for the cache or the table launch; then one launch per
+    // tree layout and mode, each stream coded by exactly one of them (tree_kind, the mark)
     switch (src) {
-    case SRC_RAW:
-        encode_kernel<0, SRC_RAW><<<grid, block, 0, st>>>(b);
-        encode_kernel<1, SRC_RAW><<<grid, block, 0, st>>>(b);
-        encode_kernel<2, SRC_RAW><<<grid, block, 0, st>>>(b);
-        break;
-    case SRC_RAW_DIFF:
-        encode_kernel<0, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
-        encode_kernel<1, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
-        encode_kernel<2, SRC_RAW_DIFF><<<grid, block, 0, st>>>(b);
-        break;
-    default:
-        encode_kernel<0, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
-        encode_kernel<1, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
-        encode_kernel<2, SRC_SYMBOLS><<<grid, block, 0, st>>>(b);
-        break;
+    case SRC_RAW: launch_encode_src<SRC_RAW>(b, grid, block, st); break;
+    case SRC_RAW_DIFF: launch_encode_src<SRC_RAW_DIFF>(b, grid, block, st); break;
+    default: launch_encode_src<SRC_SYMBOLS>(b, grid, block, st); break;
     }
     return hipGetLastError();
 }
@@ -1615,6 +1817,13 @@ extern "C" int hc_debug_set_min_tree(uint32_t kind)
 {
     // 0 narrow, 1 wide, 2 huge: the smallest tree layout of every later FGK launch
     hc::g_min_tree = kind > 2 ? 2 : kind;
+    return 0;
+}
+
+extern "C" int hc_debug_set_enc_tab(uint32_t mode)
+{
+    // 0: per stream (sampled alphabet), 1: path cache for every stream, 2: tables for every stream
+    hc::g_enc_tab = mode > 2 ? 0 : mode;
     return 0;
 }
 

@@ -301,6 +301,17 @@ def debug_set_min_tree(kind):
         raise HCodecError(f"hc_debug_set_min_tree failed: {rc}")
 
 
+def debug_set_enc_tab(mode):
+    """Test hook (not part of include/hcodec.h): how the encoder finds a symbol's code for
+    narrow / wide streams: 0 per stream from a sample of its alphabet (the default), 1 the path
+    cache for every stream, 2 the level tables for every stream."""
+    f = lib().hc_debug_set_enc_tab
+    f.argtypes = [ctypes.c_uint32]
+    rc = f(int(mode))
+    if rc:
+        raise HCodecError(f"hc_debug_set_enc_tab failed: {rc}")
+
+
 def compress_bound(n, use_adapt=False):
     return int(lib().hc_compress_bound(n, int(bool(use_adapt))))
 

@@ -38,8 +38,7 @@ enum hc_status {
     HC_ERR_LEFTOVER = 15,     /* transform.cpp:354-358  bytes left after the last block      */
     /* beyond the reference (it has no equivalent, or crashes) */
     HC_ERR_CAPACITY = 64,     /* output capacity too small; the needed length is reported    */
-    HC_ERR_UNSUPPORTED = 65,  /* -a stream given to a non-adaptive entry point or vice versa; an
-                                 adaptive matrix whose block RLE holds >= 2^32-1 symbols     */
+    HC_ERR_UNSUPPORTED = 65,  /* -a stream given to a non-adaptive entry point or vice versa */
     HC_ERR_BLOCK_SIZE = 66,   /* forged adaptive header, block size 0 (reference: SIGFPE)    */
     HC_ERR_TOO_LARGE = 67,    /* forged adaptive header, W*H > 2^36 (reference: bad_alloc)   */
     HC_ERR_DEVICE = 70,       /* HIP runtime error / no gfx950 device                        */
@@ -61,7 +60,7 @@ uint64_t hc_compress_bound(uint64_t in_len, int use_adapt);
 /* huffCompress(ifs, useDiffModel, useAdaptRLE, matrixWidth). Writes the whole stream
  * (<u64 LE count><u8 flags><FGK bits>) to out. Returns HC_OK, HC_ERR_WIDTH (width == 0, the
  * CLI check of main.cpp:195-199), HC_ERR_MATRIX_SIZE, HC_ERR_DIMS, HC_ERR_CAPACITY (out_cap <
- * result; *out_len = needed), HC_ERR_UNSUPPORTED, HC_ERR_DEVICE or HC_ERR_ARG. */
+ * result; *out_len = needed), HC_ERR_DEVICE or HC_ERR_ARG. */
 int hc_compress(const uint8_t *in, uint64_t in_len, int use_diff, int use_adapt, uint64_t width,
                 uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 
@@ -104,8 +103,8 @@ int hc_decompress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64
  * (main.cpp:39-87) for every matrix i = in[in_offs[i] .. +in_lens[i]) of width widths[i]:
  * [diff model] -> adaptive block RLE (transform.cpp:294-328: block-size search, per-block
  * scan order, header) -> FGK -> <u64 count><flags 0x40 | diff> header. Per-stream status:
- * HC_OK, HC_ERR_WIDTH (width 0), HC_ERR_MATRIX_SIZE, HC_ERR_DIMS, HC_ERR_CAPACITY,
- * HC_ERR_UNSUPPORTED. `work` is device scratch of work_bytes (16-byte aligned), at least
+ * HC_OK, HC_ERR_WIDTH (width 0), HC_ERR_MATRIX_SIZE, HC_ERR_DIMS, HC_ERR_CAPACITY.
+ * `work` is device scratch of work_bytes (16-byte aligned), at least
  * hc_adapt_compress_work_bound(sum of in_lens, n_streams); out capacity per stream:
  * hc_compress_bound(in_len, 1) always suffices.
  * ------------------------------------------------------------------------------------- */
