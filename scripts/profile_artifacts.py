@@ -30,10 +30,14 @@ FGK_SRC = os.path.join(ROOT, "huffman-codec_amd", "csrc", "hc_fgk.hip")
 
 
 def kernel_key(name):
-    """encode_kernel<0, 1> (tree layout 0 = narrow; round-1 builds: <false, 1>) ->
-    ('encode_kernel', narrow, source / destination kind)"""
-    m = re.search(r"(encode_kernel|decode_kernel)<(false|true|\d), (\d)>", name)
-    return (m.group(1), m.group(2) in ("false", "0"), int(m.group(3))) if m else None
+    """encode_kernel<0, 1, false> (tree layout 0 = narrow, source 1, path-cache mode; round-1 builds:
+    <false, 1>) -> ('encode_kernel', narrow, source / destination kind). The table-mode launch of
+    the same layout (<0, 1, true>) is keyed apart: on the -c -m headline its waves exit at once."""
+    m = re.search(r"(encode_kernel|decode_kernel)<(false|true|\d), (\d)(, (false|true))?>", name)
+    if not m:
+        return None
+    name = m.group(1) + ("_tables" if m.group(5) == "true" else "")
+    return (name, m.group(2) in ("false", "0"), int(m.group(3)))
 
 
 def main():
