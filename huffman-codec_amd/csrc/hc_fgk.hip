@@ -1218,13 +1218,20 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         const uint32_t fresh = s == 0;
         if (fresh) s = uni(fgk.split(sym));
         uint32_t pv;
-        const uint32_t d = fgk.chase(s, pv);
+        uint32_t d;
+        {
+            HC_PROF_BEGIN();
+            d = fgk.chase(s, pv);
+            HC_PROF_END(6);
+        }
         const uint64_t bits = ballot(pv & 1u);
         if (!fresh && d <= 8) {  // the tables are short of it (a split since the last build)
             if (++fgk.stale >= kRefresh) fgk.from = 0;
         }
+        HC_PROF_BEGIN();
         if (d > kInsertDepth) fgk.walk(s, pv);
         else fgk.update_path(pv);
+        HC_PROF_END(7);
         if (fresh) {
             sink.push_bits(bits >> 1, d - 1);
             sink.push((1u << 8) | sym);
@@ -1235,7 +1242,11 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     auto code_all_tab = [&](uint32_t ns) __attribute__((always_inline)) {
         uint32_t t = 0;
         while (t < ns) {
-            if (fgk.from < 9) fgk.build_levels();
+            if (fgk.from < 9) {
+                HC_PROF_BEGIN();
+                fgk.build_levels();
+                HC_PROF_END(5);
+            }
             uint32_t rl = sink.n;
             const uint32_t rend = min(64u, rl + (ns - t));
             const uint32_t x1 = vreg(fgk.T.where[sb[t + 1]]);
@@ -1281,14 +1292,22 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                 if (!ok) {  // not in the tables: nothing was stored; code it from scratch
                     --t;
                     sink.n = rl - 1;  // its record lane, overwritten by the miss path
+                    HC_PROF_BEGIN();
                     miss_tab(sb[t]);
+                    HC_PROF_END(1);
                     ++t;
                     continue;
                 }
+                HC_PROF_BEGIN();
                 fgk.walk(lane_read(pv, k), pv);
+                HC_PROF_END(2);
             }
             sink.n = rl;
-            if (rl == 64) sink.pack();
+            if (rl == 64) {
+                HC_PROF_BEGIN();
+                sink.pack();
+                HC_PROF_END(3);
+            }
         }
     };
 

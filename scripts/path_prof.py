@@ -19,6 +19,9 @@ sys.path.insert(0, os.path.join(ROOT, "huffman-codec_amd", "python"))
 ENC = {1: "miss (chase, insert, update, push)", 5: "  of which: chase", 6: "  of which: update (walk)",
        2: "walk after a failed leader test", 3: "record pack", 4: "MNP-5 chunk pass",
        7: "  of which (any walk): cache scan per swap"}
+# encoder table mode (code_all_tab; --enc-tab 2)
+TAB = {1: "miss (not in the tables)", 6: "  of which: chase", 7: "  of which: update (walk)",
+       2: "walk after a failed leader test", 3: "record pack", 4: "MNP-5 chunk pass", 5: "level table rebuild"}
 DEC = {1: "walk after a failed leader test", 2: "long code descent / NYT", 3: "update after descent / NYT",
        4: "RLE + diff revert", 5: "level table rebuild"}
 
@@ -40,6 +43,7 @@ def main():
     ap.add_argument("--streams", type=int, default=8192)
     ap.add_argument("--kind", default="photo")
     ap.add_argument("--no-diff", action="store_true")
+    ap.add_argument("--enc-tab", type=int, default=0, help="encoder mode: 0 auto, 1 cache, 2 tables")
     args = ap.parse_args()
     import torch
     import hcodec as hc
@@ -62,11 +66,12 @@ def main():
     bst = torch.zeros_like(est)
     trace = torch.zeros(8 * S, dtype=torch.int64, device=dev)
     diff = not args.no_diff
+    hc.debug_set_enc_tab(args.enc_tab)
     assert L.hc_debug_set_trace(ctypes.c_void_p(trace.data_ptr())) == 0
     try:
         hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, est, use_diff=diff)
         torch.cuda.synchronize()
-        report("encode_kernel", ENC, trace.view(S, 8).double().cpu().numpy())
+        report("encode_kernel", TAB if args.enc_tab == 2 else ENC, trace.view(S, 8).double().cpu().numpy())
         trace.zero_()
         hc.decompress_batch(enc, eoffs, elens, back, offs, lens, blens, bst)
         torch.cuda.synchronize()

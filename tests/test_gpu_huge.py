@@ -8,8 +8,9 @@ tree_kind). Coding one real stream past 2^32 symbols takes minutes per direction
 wavefront), so these tests force every stream onto the wide or the huge layout
 (hc_debug_set_min_tree) and check the kernels bit for bit on ordinary inputs: the reference's
 digests, its edge and malformed-stream vectors, the deep / skewed trees against the oracle, and
-both adaptive entry points. test_huge_real_stream (opt-in: HC_HUGE_REAL=1) codes one stream of
-2^32 + 2^20 symbols and compares it with the oracle.
+both adaptive entry points. test_huge_real_stream_encode / _decode (opt-in: HC_HUGE_REAL=enc /
+dec, ~10 minutes each on one wavefront) code one stream of 2^32 + 2^20 symbols against the
+oracle; their logs are kept under profiles/.
 """
 import hashlib
 import os
@@ -119,15 +120,19 @@ def test_header_count_past_u32(gpu, hc, oracle_mod):
     assert st == [ost] == [9]
 
 
-@pytest.mark.timeout(1100)
-@pytest.mark.skipif(os.environ.get("HC_HUGE_REAL") != "1", reason="opt-in: minutes per direction")
-def test_huge_real_stream(gpu, hc, oracle_mod):
-    """one stream of 2^32 + 2^20 FGK symbols (-c on a 4 GiB input without runs of 3): encoded
-    byte for byte like the oracle (u64 weights), round trip exact"""
-    torch = gpu
+def _huge_input(torch):
     n = (1 << 32) + (1 << 20)
     pat = torch.tensor([1, 1, 2, 1, 1, 3, 1, 1, 2], dtype=torch.uint8, device="cuda")
-    raw = pat.repeat(n // pat.numel() + 1)[:n].contiguous()
+    return n, pat.repeat(n // pat.numel() + 1)[:n].contiguous()
+
+
+@pytest.mark.timeout(1100)
+@pytest.mark.skipif(os.environ.get("HC_HUGE_REAL") != "enc", reason="opt-in: ~10 minutes on one wavefront")
+def test_huge_real_stream_encode(gpu, hc, oracle_mod):
+    """one stream of 2^32 + 2^20 FGK symbols (-c on a 4 GiB input without runs of 3, so every
+    byte is a symbol): the GPU encoding is byte for byte the oracle's (u64 weights)"""
+    torch = gpu
+    n, raw = _huge_input(torch)
     cap = n // 2
     enc = torch.zeros(cap, dtype=torch.uint8, device="cuda")
     i64 = dict(dtype=torch.int64, device="cuda")
@@ -138,16 +143,30 @@ def test_huge_real_stream(gpu, hc, oracle_mod):
     torch.cuda.synchronize()
     assert est.item() == 0
     got = enc[:elen.item()].cpu().numpy()
-    assert int.from_bytes(got[:8].tobytes(), "little") == n  # every byte a symbol: no runs of 3
+    assert int.from_bytes(got[:8].tobytes(), "little") == n  # every byte a symbol
     host = raw.cpu().numpy()
+    del raw
     want_st, want = oracle_mod.compress(host, False, False, 512)
-    del host
     assert want_st == 0 and len(want) == len(got) and np.array_equal(np.frombuffer(want, np.uint8), got)
-    del want, got
+
+
+@pytest.mark.timeout(1100)
+@pytest.mark.skipif(os.environ.get("HC_HUGE_REAL") != "dec", reason="opt-in: ~12 minutes on one wavefront")
+def test_huge_real_stream_decode(gpu, hc, oracle_mod):
+    """the oracle's encoding of the same 2^32 + 2^20-symbol stream decoded on the GPU (huge tree
+    layout picked from the header count): exactly the input"""
+    torch = gpu
+    n, raw = _huge_input(torch)
+    want_st, want = oracle_mod.compress(raw.cpu().numpy(), False, False, 512)
+    assert want_st == 0 and int.from_bytes(want[:8], "little") == n
+    enc = torch.from_numpy(np.frombuffer(want, np.uint8).copy()).cuda()
+    del want
+    i64 = dict(dtype=torch.int64, device="cuda")
+    z = torch.zeros(1, **i64)
     back = torch.zeros_like(raw)
     blen = torch.zeros(1, **i64)
     bst = torch.full((1,), -1, dtype=torch.int32, device="cuda")
-    hc.decompress_batch(enc, z, elen, back, z, torch.tensor([n], **i64), blen, bst)
+    hc.decompress_batch(enc, z, torch.tensor([enc.numel()], **i64), back, z, torch.tensor([n], **i64), blen, bst)
     torch.cuda.synchronize()
     assert bst.item() == 0 and blen.item() == n
     assert torch.equal(back, raw)
