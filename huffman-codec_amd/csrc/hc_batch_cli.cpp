@@ -7,9 +7,9 @@
 //
 // Compression writes FILE.huf, decompression FILE without its .huf suffix (else FILE.out);
 // with -o into OUTDIR under the same base name. Files are read and written by a pool of
-// THREADS host threads (default 8). -a (adaptive block RLE, one matrix per file) codes the
-// files one by one through hc_compress / hc_decompress; everything else goes through
-// hc_compress_host_batch / hc_decompress_host_batch in one call. A file that fails reports
+// THREADS host threads (default 8). All files go through the pipelined host-batch API in one
+// call: hc_compress_host_batch, hc_compress_adapt_host_batch (-a: one matrix of width WIDTH per
+// file) or hc_decompress_host_batch (any mix of adaptive and plain streams). A file that fails reports
 // "FILE: <the reference's message>"; the exit code is the first failing status (0: all ok).
 #include <unistd.h>
 
@@ -117,28 +117,23 @@ int main(int argc, char *argv[])
         in[i].assign(std::istreambuf_iterator<char>(ifs), std::istreambuf_iterator<char>());
     });
 
-    if (use_adapt && compress) {  // one matrix per file: the single-buffer path
-        for (size_t i = 0; i < n; ++i) {
-            if (status[i]) continue;
-            out[i].resize(hc_compress_bound(in[i].size(), 1));
-            uint64_t len = 0;
-            status[i] = hc_compress(in[i].data(), in[i].size(), use_diff, 1, width, out[i].data(), out[i].size(), &len);
-            out[i].resize(status[i] ? 0 : len);
-        }
-    } else if (compress) {
+    if (compress) {  // -a: one matrix of width `width` per file
         std::vector<const uint8_t *> ip(n);
         std::vector<uint8_t *> op(n);
-        std::vector<uint64_t> il(n), oc(n), ol(n);
+        std::vector<uint64_t> il(n), oc(n), ol(n), wd(n, width);
         std::vector<int32_t> st(n, 0);
         for (size_t i = 0; i < n; ++i) {
             ip[i] = in[i].data();
             il[i] = status[i] ? 0 : in[i].size();
-            out[i].resize(hc_compress_bound(il[i], 0));
+            out[i].resize(hc_compress_bound(il[i], use_adapt));
             op[i] = out[i].data();
             oc[i] = out[i].size();
         }
-        const int rc = hc_compress_host_batch(ip.data(), il.data(), (uint32_t)n, use_diff ? HC_FLAG_DIFF : 0, op.data(),
-                                              oc.data(), ol.data(), st.data());
+        const uint32_t fl = use_diff ? HC_FLAG_DIFF : 0;
+        const int rc = use_adapt ? hc_compress_adapt_host_batch(ip.data(), il.data(), wd.data(), (uint32_t)n, fl,
+                                                                op.data(), oc.data(), ol.data(), st.data())
+                                 : hc_compress_host_batch(ip.data(), il.data(), (uint32_t)n, fl, op.data(), oc.data(),
+                                                          ol.data(), st.data());
         if (rc) {
             std::cerr << hc_status_message(rc);
             return rc;
@@ -148,21 +143,11 @@ int main(int argc, char *argv[])
             out[i].resize(status[i] ? 0 : ol[i]);
         }
     } else {
-        // adaptive streams (flags bit 6) go one by one; the rest in one batch, whose output
-        // sizes are unknown up front: a guess, then the exact size for those that report it
+        // one batch (adaptive and plain streams alike), whose output sizes are unknown up
+        // front: a guess, then the exact size for those that report it
         std::vector<size_t> batch;
-        for (size_t i = 0; i < n; ++i) {
-            if (status[i]) continue;
-            if (in[i].size() >= 9 && (in[i][8] & HC_FLAG_ADAPT)) {
-                uint8_t *p = nullptr;
-                uint64_t len = 0;
-                status[i] = hc_decompress_alloc(in[i].data(), in[i].size(), &p, &len);
-                if (!status[i]) out[i].assign(p, p + len);
-                hc_free(p);
-            } else {
-                batch.push_back(i);
-            }
-        }
+        for (size_t i = 0; i < n; ++i)
+            if (!status[i]) batch.push_back(i);
         for (int pass = 0; pass < 2 && !batch.empty(); ++pass) {
             const size_t m = batch.size();
             std::vector<const uint8_t *> ip(m);

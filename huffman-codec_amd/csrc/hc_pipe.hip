@@ -101,7 +101,7 @@ struct Slot {
     hipEvent_t meta_done = nullptr;
     Pinned<uint8_t> hin, hpacked;
     Pinned<uint64_t> hup, hdown;
-    Dev<uint8_t> din, dout, dpacked, dtmp;
+    Dev<uint8_t> din, dout, dpacked, dtmp, dwork;
     Dev<uint64_t> dup, dlens, dkept, dat;
     Dev<int32_t> dstatus;
     uint32_t first = 0, count = 0;  // streams [first, first + count) of the call
@@ -115,6 +115,8 @@ struct Slot {
 
 struct Job {
     bool encode;
+    bool adapt;              // -a streams: the batched adaptive device API (widths: encode only)
+    const uint64_t *widths;
     uint32_t flags;
     const uint8_t *const *in;
     const uint64_t *in_lens;
@@ -133,7 +135,7 @@ uint64_t guess_cap(const Job &j, uint32_t i)
     const uint64_t n = j.in_lens[i];
     uint64_t c;
     if (j.encode) {
-        c = n + n / 4 + 4096;
+        c = j.adapt ? hc_compress_bound(n, 1) : n + n / 4 + 4096;
     } else {
         uint64_t count = 0;
         if (n >= 9)
@@ -153,13 +155,14 @@ int launch(Job &j, Slot &s)
         in_bytes += up16(j.in_lens[s.first + k]);
         out_bytes += up16(j.dcap[s.first + k]);
     }
+    const uint64_t cols = j.adapt && j.encode ? 5 : 4;  // + the widths column
     PIPE_CK(s.hin.need(in_bytes));
-    PIPE_CK(s.hup.need(4ull * n));
+    PIPE_CK(s.hup.need(cols * n));
     PIPE_CK(s.hdown.need(3ull * n + 1));
     PIPE_CK(s.din.need(in_bytes));
     PIPE_CK(s.dout.need(out_bytes));
     PIPE_CK(s.dpacked.need(out_bytes));
-    PIPE_CK(s.dup.need(4ull * n));
+    PIPE_CK(s.dup.need(cols * n));
     PIPE_CK(s.dlens.need(n));
     PIPE_CK(s.dkept.need(n));
     PIPE_CK(s.dat.need(n + 1));
@@ -175,17 +178,27 @@ int launch(Job &j, Slot &s)
         up[n + k] = len;
         up[2 * n + k] = oo;
         up[3 * n + k] = j.dcap[i];
+        if (cols == 5) up[4 * n + k] = j.widths[i];
         io += up16(len);
         oo += up16(j.dcap[i]);
     }
     PIPE_CK(hipMemcpyAsync(s.din.p, s.hin.p, in_bytes, hipMemcpyHostToDevice, s.st));
-    PIPE_CK(hipMemcpyAsync(s.dup.p, up, 4ull * n * sizeof(uint64_t), hipMemcpyHostToDevice, s.st));
+    PIPE_CK(hipMemcpyAsync(s.dup.p, up, cols * n * sizeof(uint64_t), hipMemcpyHostToDevice, s.st));
     const uint64_t *d = s.dup.p;
     hc::Batch b{s.din.p, d, d + n, n, s.dout.p, d + 2 * n, d + 3 * n, s.dlens.p, s.dstatus.p, j.flags};
-    if (j.encode)
+    if (j.adapt) {  // workspace of the adaptive stages, sized for this sub-batch
+        const uint64_t wb = j.encode ? hc::adapt_encode_work_bound(in_bytes, n)
+                                     : hc::adapt_decode_work_bound(in_bytes, out_bytes, n);
+        PIPE_CK(s.dwork.need(wb));
+        if (j.encode)
+            PIPE_CK(hc::adapt_encode_batch(b, d + 4 * n, s.dwork.p, s.dwork.cap, s.st));
+        else
+            PIPE_CK(hc::adapt_decode_batch(b, s.dwork.p, s.dwork.cap, s.st));
+    } else if (j.encode) {
         PIPE_CK(hc::launch_encode(b, (j.flags & HC_FLAG_DIFF) ? hc::SRC_RAW_DIFF : hc::SRC_RAW, s.st));
-    else
+    } else {
         PIPE_CK(hc::launch_decode(b, hc::DST_RAW, s.st));
+    }
     // compaction: kept lengths, their exclusive scan (+ total), the copy
     kept_lengths<<<(n + 255) / 256, 256, 0, s.st>>>(s.dlens.p, s.dstatus.p, s.dkept.p, n);
     size_t tb = 0;
@@ -312,7 +325,16 @@ int hc_compress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, ui
                            uint64_t *out_lens, int32_t *status)
 {
     if (flags & ~HC_FLAG_DIFF) return HC_ERR_ARG;
-    Job j{true, flags, in, in_lens, out, out_caps, out_lens, status, {}};
+    Job j{true, false, nullptr, flags, in, in_lens, out, out_caps, out_lens, status, {}};
+    return run(j, n_streams);
+}
+
+int hc_compress_adapt_host_batch(const uint8_t *const *in, const uint64_t *in_lens, const uint64_t *widths,
+                                 uint32_t n_streams, uint32_t flags, uint8_t *const *out, const uint64_t *out_caps,
+                                 uint64_t *out_lens, int32_t *status)
+{
+    if ((flags & ~HC_FLAG_DIFF) || (n_streams && !widths)) return HC_ERR_ARG;
+    Job j{true, true, widths, flags, in, in_lens, out, out_caps, out_lens, status, {}};
     return run(j, n_streams);
 }
 
@@ -330,8 +352,41 @@ int hc_decompress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, 
                              uint8_t *const *out, const uint64_t *out_caps, uint64_t *out_lens,
                              int32_t *status)
 {
-    Job j{false, 0, in, in_lens, out, out_caps, out_lens, status, {}};
-    return run(j, n_streams);
+    if (n_streams && (!in || !in_lens)) return HC_ERR_ARG;
+    // adaptive streams (flags bit 6) and the rest go through their own device paths, each as
+    // one job over the streams of its kind (gathered, results scattered back)
+    std::vector<uint32_t> ids[2];
+    for (uint32_t i = 0; i < n_streams; ++i) {
+        const bool a = in_lens[i] >= 9 && in[i] && (in[i][8] & HC_FLAG_ADAPT);
+        ids[a].push_back(i);
+    }
+    for (int a = 0; a < 2; ++a) {
+        const std::vector<uint32_t> &id = ids[a];
+        if (id.empty()) continue;
+        if (id.size() == n_streams) {
+            Job j{false, a == 1, nullptr, 0, in, in_lens, out, out_caps, out_lens, status, {}};
+            return run(j, n_streams);
+        }
+        const size_t m = id.size();
+        std::vector<const uint8_t *> ip(m);
+        std::vector<uint8_t *> op(m);
+        std::vector<uint64_t> il(m), oc(m), ol(m, 0);
+        std::vector<int32_t> st(m, 0);
+        for (size_t k = 0; k < m; ++k) {
+            ip[k] = in[id[k]];
+            il[k] = in_lens[id[k]];
+            op[k] = out ? out[id[k]] : nullptr;
+            oc[k] = out_caps ? out_caps[id[k]] : 0;
+        }
+        Job j{false, a == 1, nullptr, 0, ip.data(), il.data(), op.data(), oc.data(), ol.data(), st.data(), {}};
+        const int rc = run(j, (uint32_t)m);
+        if (rc) return rc;
+        for (size_t k = 0; k < m; ++k) {
+            if (out_lens) out_lens[id[k]] = ol[k];
+            if (status) status[id[k]] = st[k];
+        }
+    }
+    return HC_OK;
 }
 
 }  // extern "C"

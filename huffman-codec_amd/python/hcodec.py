@@ -81,6 +81,7 @@ def lib():
     L.hc_decompress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
     L.hc_compress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp]
     L.hc_decompress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, vp, vp, vp, vp]
+    L.hc_compress_adapt_host_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp]
     L.hc_adapt_compress_work_bound.argtypes = [u64, ctypes.c_uint32]
     L.hc_adapt_compress_work_bound.restype = u64
     L.hc_adapt_decompress_work_bound.argtypes = [u64, u64, ctypes.c_uint32]
@@ -264,6 +265,19 @@ def compress_host_batch(blobs, use_diff=False, caps=None):
     """hc_compress_host_batch on host byte strings: (statuses, encoded, out_lens)."""
     caps = caps if caps is not None else [compress_bound(len(b)) for b in blobs]
     return _host_batch(lib().hc_compress_host_batch, blobs, caps, HC_FLAG_DIFF if use_diff else 0)
+
+
+def compress_adapt_host_batch(blobs, widths, use_diff=False, caps=None):
+    """hc_compress_adapt_host_batch on host byte strings (-a, one matrix of widths[i] per blob):
+    (statuses, encoded, out_lens)."""
+    caps = caps if caps is not None else [compress_bound(len(b), True) for b in blobs]
+    w = (ctypes.c_uint64 * max(len(blobs), 1))(*[int(x) for x in widths])
+    L = lib()
+
+    def fn(ins, lens, n, outs, ocaps, olens, st):
+        return L.hc_compress_adapt_host_batch(ins, lens, ctypes.cast(w, ctypes.c_void_p), n,
+                                              HC_FLAG_DIFF if use_diff else 0, outs, ocaps, olens, st)
+    return _host_batch(fn, blobs, caps)
 
 
 def decompress_host_batch(blobs, caps):

@@ -137,14 +137,21 @@ int hc_decompress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const 
  * (default 8192). The return value reports argument / device errors only.
  * ------------------------------------------------------------------------------------- */
 
-/* flags: 0 or HC_FLAG_DIFF (adaptive streams go through hc_compress). out_caps[i] >=
+/* flags: 0 or HC_FLAG_DIFF (adaptive: hc_compress_adapt_host_batch). out_caps[i] >=
  * hc_compress_bound(in_lens[i], 0) always suffices. */
 int hc_compress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, uint32_t n_streams,
                            uint32_t flags, uint8_t *const *out, const uint64_t *out_caps,
                            uint64_t *out_lens, int32_t *status);
 
-/* Non-adaptive streams (flags bit 6 clear; others get HC_ERR_UNSUPPORTED: use
- * hc_decompress). */
+/* The same for adaptive (-a) matrices: huffCompress(ifs, useDiff, true, widths[i]) for every
+ * matrix (main.cpp:39-87) through the batched adaptive device API, pipelined in sub-batches
+ * like hc_compress_host_batch. Status per stream as hc_compress_adapt_batch. */
+int hc_compress_adapt_host_batch(const uint8_t *const *in, const uint64_t *in_lens, const uint64_t *widths,
+                                 uint32_t n_streams, uint32_t flags, uint8_t *const *out, const uint64_t *out_caps,
+                                 uint64_t *out_lens, int32_t *status);
+
+/* Any streams: adaptive ones (flags bit 6) through the batched adaptive device path, the rest
+ * through the FGK -> RLE revert -> [diff revert] path, each kind pipelined in sub-batches. */
 int hc_decompress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, uint32_t n_streams,
                              uint8_t *const *out, const uint64_t *out_caps, uint64_t *out_lens,
                              int32_t *status);

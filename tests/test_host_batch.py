@@ -1,6 +1,7 @@
-"""Host-buffer batches (hc_compress_host_batch / hc_decompress_host_batch, csrc/hc_pipe.hip) and
-the `huffman-codec-batch` tool: byte-identical to the oracle (the reference's algorithm) per
-stream, through the pipelined sub-batches. SURVEY.md §8f-1."""
+"""Host-buffer batches (hc_compress_host_batch / hc_compress_adapt_host_batch /
+hc_decompress_host_batch, csrc/hc_pipe.hip) and the `huffman-codec-batch` tool: byte-identical to
+the oracle (the reference's algorithm) per stream, through the pipelined sub-batches, adaptive
+(-a) matrices included. SURVEY.md §8f-1."""
 import os
 import subprocess
 
@@ -45,7 +46,7 @@ def test_host_batch_statuses(gpu, hc, oracle_mod):
     assert st[0] == 0 and dec[0] == raw
     assert st[1] == ref[1] == hc.HC_ERR_HEADER
     assert st[2] == ref[2] == hc.HC_ERR_HUFFMAN
-    assert st[3] == hc.HC_ERR_UNSUPPORTED  # adaptive: hc_decompress
+    assert st[3] == 0 and dec[3] == raw  # adaptive: through the batched adaptive path
     assert st[4] == hc.HC_ERR_CAPACITY and lens[4] == len(raw)  # too small: the size it needs
     # compress: a capacity below the result reports the needed length
     st, _, lens = hc.compress_host_batch([raw], use_diff=True, caps=[16])
@@ -79,17 +80,47 @@ def test_batch_cli_matches_oracle(gpu, hc, oracle_mod, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("slots", ["default", "tiny"])
+@pytest.mark.parametrize("use_diff", [False, True])
+def test_adapt_host_batch_vs_oracle(gpu, hc, oracle_mod, use_diff, slots, monkeypatch):
+    """-a matrices of several widths (and the reference's failures: width 0 -> 4, a size not a
+    multiple of the width -> 6, a side below 8 -> 12) through hc_compress_adapt_host_batch, then
+    decoded together with plain streams by hc_decompress_host_batch"""
+    if slots == "tiny":
+        monkeypatch.setenv("HC_PIPE_STREAMS", "2")
+        monkeypatch.setenv("HC_PIPE_BYTES", "40000")
+    mats = [(oracle_mod.synth("photo", k, w, h).tobytes(), w) for k, (w, h) in
+            enumerate([(64, 64), (100, 37), (512, 512), (8, 8), (200, 129)])]
+    mats += [(oracle_mod.synth("grad", 1, 96, 64).tobytes(), 96), (oracle_mod.synth("noise", 2, 40, 40).tobytes(), 40)]
+    mats += [(b"x" * 640, 0), (b"y" * 650, 64), (b"z" * 640, 128)]  # statuses 4, 6, 12
+    raws, widths = [m[0] for m in mats], [m[1] for m in mats]
+    st, enc, _ = hc.compress_adapt_host_batch(raws, widths, use_diff=use_diff)
+    for r, w, s, e in zip(raws, widths, st, enc):
+        ws, want = oracle_mod.compress(r, use_diff, True, w) if w else (hc.HC_ERR_WIDTH, b"")
+        assert s == ws and (s != 0 or e == want), (len(r), w)
+    ok = [i for i, s in enumerate(st) if s == 0]
+    plain = [oracle_mod.compress(raws[0], True, False, 512)[1]]
+    blobs = [enc[i] for i in ok] + plain
+    dst, dec, _ = hc.decompress_host_batch(blobs, [len(raws[i]) + 16 for i in ok] + [len(raws[0])])
+    assert dst == [0] * len(blobs) and dec == [raws[i] for i in ok] + [raws[0]]
+
+
+@pytest.mark.gpu
 def test_batch_cli_adaptive(gpu, hc, oracle_mod, tmp_path):
-    raw = oracle_mod.synth("photo", 3, 64, 64).tobytes()
-    f = tmp_path / "m.raw"
-    f.write_bytes(raw)
-    p = subprocess.run([hc.BATCH_CLI_PATH, "-c", "-a", "-m", "-w", "64", str(f)], capture_output=True, text=True)
+    raws = [oracle_mod.synth("photo", k, 64, 48).tobytes() for k in range(4)]
+    files = []
+    for k, raw in enumerate(raws):
+        f = tmp_path / f"m{k}.raw"
+        f.write_bytes(raw)
+        files.append(str(f))
+    p = subprocess.run([hc.BATCH_CLI_PATH, "-c", "-a", "-m", "-w", "64"] + files, capture_output=True, text=True)
     assert p.returncode == 0, p.stderr
-    enc = (tmp_path / "m.raw.huf").read_bytes()
-    assert enc == oracle_mod.compress(raw, True, True, 64)[1]
-    p = subprocess.run([hc.BATCH_CLI_PATH, "-d", str(tmp_path / "m.raw.huf")], capture_output=True, text=True)
+    for f, raw in zip(files, raws):
+        assert open(f + ".huf", "rb").read() == oracle_mod.compress(raw, True, True, 64)[1]
+    p = subprocess.run([hc.BATCH_CLI_PATH, "-d"] + [f + ".huf" for f in files], capture_output=True, text=True)
     assert p.returncode == 0, p.stderr
-    assert (tmp_path / "m.raw").read_bytes() == raw
+    for f, raw in zip(files, raws):
+        assert open(f, "rb").read() == raw
 
 
 def test_batch_cli_arguments(hc):
