@@ -1212,6 +1212,35 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     auto path_read = [&](uint32_t pcw) __attribute__((always_inline)) {
         return opaque(*(const lds_u16 *)(size_t)(pbase + ((pcw & 255u) >> psh) * 2));
     };
+    // the root path of position s0 (lane k: level k, kRoot above): climb parent links until a
+    // position that pcode[] puts at depth 8 and the tables confirm; the tables give the other 8
+    // levels in one read (a 10-bit code: 2 climbs instead of 10). Returns the depth.
+    auto chase_tab = [&](uint32_t s0, uint32_t &pv) __attribute__((always_inline)) -> uint32_t {
+        uint32_t s = s0, n = 0, td = kRoot;  // td lane j: level n - 1 - j
+        for (;;) {
+            const uint32_t pc = uni(fgk.T.pcode[s]);
+            const uint32_t par = fgk.parent(s);
+            if (((pc >> 8) & 7u) == 7u) {
+                const uint32_t pr = path_read(pc);
+                if (uni(pr) == (s | (8u << 10))) {
+                    const uint32_t dn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((n - 1 - lane) & 63u) * 4), (int)td);
+                    const uint32_t tb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - n) & 63u) * 4), (int)pr);
+                    pv = lane < n ? dn : (lane - n < 9 ? (tb & 1023u) : kRoot);
+                    return n + 8;
+                }
+            }
+            const uint32_t sh = __builtin_amdgcn_update_dpp(0u, td, 0x138, 0xF, 0xF, true);
+            td = lane == 0 ? s : sh;
+            ++n;
+            if (par == kRoot || n >= 63) {  // the root, or (a bug) a cycle
+                fgk.bad |= par ^ kRoot;
+                const uint32_t dn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((n - 1 - lane) & 63u) * 4), (int)td);
+                pv = lane < n ? dn : kRoot;
+                return n;
+            }
+            s = par;
+        }
+    };
     auto miss_tab = [&](uint32_t sv) {
         const uint32_t sym = uni(sv);
         uint32_t s = uni(fgk.T.where[sym]) & 1023u;
@@ -1221,7 +1250,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         uint32_t d;
         {
             HC_PROF_BEGIN();
-            d = fgk.chase(s, pv);
+            d = chase_tab(s, pv);
             HC_PROF_END(6);
         }
         const uint64_t bits = ballot(pv & 1u);
