@@ -14,6 +14,7 @@ oracle; their logs are kept under profiles/.
 """
 import hashlib
 import os
+import time
 
 import numpy as np
 import pytest
@@ -139,14 +140,18 @@ def test_huge_real_stream_encode(gpu, hc, oracle_mod):
     z = torch.zeros(1, **i64)
     elen = torch.zeros(1, **i64)
     est = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    t0 = time.time()
     hc.compress_batch(raw, z, torch.tensor([n], **i64), enc, z, torch.tensor([cap], **i64), elen, est)
     torch.cuda.synchronize()
+    print(f"gpu encode {time.time() - t0:.1f} s", flush=True)
     assert est.item() == 0
     got = enc[:elen.item()].cpu().numpy()
     assert int.from_bytes(got[:8].tobytes(), "little") == n  # every byte a symbol
     host = raw.cpu().numpy()
     del raw
+    t0 = time.time()
     want_st, want = oracle_mod.compress(host, False, False, 512)
+    print(f"oracle encode {time.time() - t0:.1f} s", flush=True)
     assert want_st == 0 and len(want) == len(got) and np.array_equal(np.frombuffer(want, np.uint8), got)
 
 
@@ -157,7 +162,9 @@ def test_huge_real_stream_decode(gpu, hc, oracle_mod):
     layout picked from the header count): exactly the input"""
     torch = gpu
     n, raw = _huge_input(torch)
+    t0 = time.time()
     want_st, want = oracle_mod.compress(raw.cpu().numpy(), False, False, 512)
+    print(f"oracle encode {time.time() - t0:.1f} s", flush=True)
     assert want_st == 0 and int.from_bytes(want[:8], "little") == n
     enc = torch.from_numpy(np.frombuffer(want, np.uint8).copy()).cuda()
     del want
@@ -166,7 +173,9 @@ def test_huge_real_stream_decode(gpu, hc, oracle_mod):
     back = torch.zeros_like(raw)
     blen = torch.zeros(1, **i64)
     bst = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    t0 = time.time()
     hc.decompress_batch(enc, z, torch.tensor([enc.numel()], **i64), back, z, torch.tensor([n], **i64), blen, bst)
     torch.cuda.synchronize()
+    print(f"gpu decode {time.time() - t0:.1f} s", flush=True)
     assert bst.item() == 0 and blen.item() == n
     assert torch.equal(back, raw)
