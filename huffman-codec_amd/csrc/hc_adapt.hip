@@ -552,9 +552,10 @@ __device__ __forceinline__ TileAt tile_at(const EncArgs &a, const Ws &ws, uint64
 // it works on the current one: tile_fetch issues the raw dword loads (coalesced along each row;
 // one aligned load per dword when the rows are dword-aligned, as in every 512-wide batch), one
 // item per thread and u ((kTile + 8) / 4 dwords x (kTile + 1) rows <= kLU x 256); tile_put
-// stores them and applies the diff model in LDS (each dword's previous byte is the byte before
-// it in the row image; only byte 3 of a row's first dword, x = tx0 - 1, is ever read, and it
-// needs just its own byte 2).
+// applies the diff model in registers and stores them (each dword's previous byte is the top
+// byte of the item before it, the dword before in the row image; a row's first dword takes a
+// stray one, harmless: only its byte 3, x = tx0 - 1, is ever read, and that needs just its own
+// byte 2).
 constexpr uint32_t kLU = ((kTile + 1) * ((kTile + 8) / 4) + 255) / 256;
 __device__ __forceinline__ void tile_fetch(const TileAt &g, uint32_t *v, uint32_t tid)
 {
@@ -571,31 +572,30 @@ __device__ __forceinline__ void tile_fetch(const TileAt &g, uint32_t *v, uint32_
         v[u] = whole ? *reinterpret_cast<const uint32_t *>(g.mat + lin) : (on ? load4(g.mat, lin, g.n) : 0u);
     }
 }
-__device__ __forceinline__ void tile_put(uint8_t *D, const TileAt &g, uint32_t *v, bool diff, uint32_t tid)
+__device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileAt &g, uint32_t *v, bool diff,
+                                         uint32_t tid)
 {
     const uint32_t nd = (g.tw + 7) / 4, items = (g.th + 1) * nd;
-    uint32_t at[kLU];  // the items' LDS byte offsets (kDS * r + 4 d), or ~0 past the image
-    {
-        TileWalk wk(nd, tid);
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    if (diff) {
+        // the previous item's dword is lane - 1's (wave_shr 1); a wave's lane 0 takes it from the
+        // lane 63 before it through edge[] (item u * 256 + tid - 1)
+        if (lane == 63) {
 #pragma unroll
-        for (uint32_t u = 0; u < kLU; ++u, wk.next())
-            at[u] = u * 256 + tid < items ? wk.r * kDS + 4 * wk.d : ~0u;
+            for (uint32_t u = 0; u < kLU; ++u) edge[4 * u + wv] = v[u];
+        }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t u = 0; u < kLU; ++u) {
+            uint32_t pv = lane_shr1(v[u], 0u);
+            if (lane == 0) pv = wv ? edge[4 * u + wv - 1] : (u ? edge[4 * u - 1] : 0u);
+            v[u] = sub8(v[u], (v[u] << 8) | (pv >> 24));
+        }
     }
+    TileWalk wk(nd, tid);
 #pragma unroll
-    for (uint32_t u = 0; u < kLU; ++u)
-        if (at[u] != ~0u) *reinterpret_cast<uint32_t *>(D + at[u]) = v[u];
-    lds_barrier();
-    if (!diff) return;
-#pragma unroll
-    for (uint32_t u = 0; u < kLU; ++u) {
-        // a row's first dword (at % kDS == 0) needs no byte before it (only its byte 3 is read)
-        const uint32_t pb = (at[u] != ~0u && at[u] % kDS != 0) ? D[at[u] - 1] : 0u;
-        v[u] = sub8(v[u], (v[u] << 8) | pb);
-    }
-    lds_barrier();
-#pragma unroll
-    for (uint32_t u = 0; u < kLU; ++u)
-        if (at[u] != ~0u) *reinterpret_cast<uint32_t *>(D + at[u]) = v[u];
+    for (uint32_t u = 0; u < kLU; ++u, wk.next())
+        if (u * 256 + tid < items) *reinterpret_cast<uint32_t *>(D + wk.r * kDS + 4 * wk.d) = v[u];
     lds_barrier();
 }
 
@@ -641,13 +641,188 @@ __device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64
     }
 }
 
+// the value of lane l + d (d a power of two): DPP row_shl inside 16-lane rows, else a permute
+__device__ __forceinline__ uint32_t shl_down(uint32_t v, uint32_t d)
+{
+    switch (d) {
+    case 1: return dpp<0x101>(v, 0u);
+    case 2: return dpp<0x102>(v, 0u);
+    case 4: return dpp<0x104>(v, 0u);
+    case 8: return dpp<0x108>(v, 0u);
+    default: return __shfl_down(v, d, 64);
+    }
+}
+
+// llvm.amdgcn.writelane (no clang builtin in this toolchain; bound by name as in hc_fgk.hip)
+extern "C" __device__ int amdgcn_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
+
+// Whole 128 x 128 tiles, B <= 64: the first bit of every block line's scan (transform.cpp:66-94:
+// the comparison across the scan's line wrap, 0 on a block's first line), as 128-bit masks over
+// the tile's lines, per candidate c and block column (h) / block row (v) b:
+// WM[o][32 - (32 >> c) + b] (31 per order). One wave per order and half of the lines (lane =
+// line): the 16 first and 16 last values of its 8-wide steps give all 31 comparisons.
+__device__ __forceinline__ void wrap_masks(const uint8_t *D, uint64_t *WM, uint32_t wv, uint32_t lane)
+{
+    const uint32_t o = wv >> 1, half = wv & 1, line = 64 * half + lane;
+    // h: DT(y + 1, 8k), DT(y, 8k + 7); v: DT(8k + 1, x), DT(8k + 8, x - 1)
+    const uint8_t *fp = D + (o ? kDS + 4 + line : (line + 1) * kDS + 4);
+    const uint8_t *lp = D + (o ? 8 * kDS + 3 + line : line * kDS + 11);
+    const uint32_t st = o ? 8 * kDS : 8u;
+    uint32_t mlo = 0, mhi = 0;  // lane i: mask i
+    auto put = [&](uint32_t i, bool eq, uint32_t B) __attribute__((always_inline)) {
+        const uint64_t m = ballot(eq && (line & (B - 1)) != 0);
+        mlo = (uint32_t)amdgcn_writelane((int)(uint32_t)m, (int)i, (int)mlo);
+        mhi = (uint32_t)amdgcn_writelane((int)(uint32_t)(m >> 32), (int)i, (int)mhi);
+    };
+    // two halves of 8 steps (B <= 64 pairs stay inside one), 16 values live at a time
+    uint32_t f0 = 0;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        uint32_t f[8], l[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            f[k] = fp[(8 * h + k) * st];
+            l[k] = lp[(8 * h + k) * st];
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) {
+            const uint32_t s = 1u << c;  // B / 8
+#pragma unroll
+            for (uint32_t b = 0; b < (8u >> c); ++b)
+                put(32 - (32 >> c) + (8u >> c) * h + b, f[b * s] == l[b * s + s - 1], 8 * s);
+        }
+        if (h == 0) f0 = f[0];
+        else put(30, f0 == l[7], 128);
+    }
+    if (lane < 31) WM[(o * 32 + lane) * 2 + half] = (uint64_t)mhi << 32 | mlo;
+}
+
+// Whole 128 x 128 tiles, B = 8 << c <= 64: the (h, v) cost of every block into hv. One 64-bit
+// word of a block's scan per thread and order (64 / B block lines from 8-, 16-, 32- or 64-bit
+// reads of the Eh / Ev rows, first bits from WM); v blocks are taken column-major so a wave's
+// lanes read few distinct words. The MNP-5 length is a pattern count over the scan (a run of L
+// costs 1 + [L >= 2] + 2 [L >= 3], counted at its first element with a two-bit look-ahead into
+// the next word), summed over the block's lanes, plus the last run's rule (run_cost(L - 1) + 1,
+// from the block's last zero bit) — exact while no run reaches 259 elements, which needs an
+// all-ones word; a wave holding one (B >= 32) folds the run-segment monoid instead.
+template <uint32_t c>
+__device__ __forceinline__ void fast_cost(const uint64_t *E, const uint64_t *WM, uint32_t *hv, uint32_t tid,
+                                          uint32_t lane)
+{
+    constexpr uint32_t B = 8u << c, lg = 3 + c;
+    constexpr uint32_t lnb = 7 - lg;       // log2 blocks per tile side
+    constexpr uint32_t lwpb = 2 * lg - 6;  // log2 words per block
+    constexpr uint32_t G = 1u << lwpb;
+    constexpr uint32_t lpw = 64 >> lg;  // block lines per word
+    constexpr uint64_t FM = c == 0 ? 0x0101010101010101ull : c == 1 ? 0x0001000100010001ull : c == 2 ? 0x0000000100000001ull : 1ull;
+    const uint8_t *Eb = reinterpret_cast<const uint8_t *>(E);
+    const uint8_t *Mb = reinterpret_cast<const uint8_t *>(WM);
+    const uint32_t blk = tid >> lwpb, j = tid & (G - 1);
+    const uint32_t bmin = blk & ((1u << lnb) - 1), bmaj = blk >> lnb;
+#pragma unroll
+    for (uint32_t o = 0; o < 2; ++o) {
+        const uint32_t bx = o ? bmaj : bmin, by = o ? bmin : bmaj;
+        const uint32_t l0 = ((o ? bx : by) << lg) + j * lpw, c0 = (o ? by : bx) << lg;
+        const uint8_t *rp = Eb + o * 16 * kTile + l0 * 16 + (c0 >> 3);
+        uint64_t word = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < lpw; ++q) {
+            uint64_t v;
+            if constexpr (c == 0) v = rp[16 * q];
+            else if constexpr (c == 1) v = *reinterpret_cast<const uint16_t *>(rp + 16 * q);
+            else if constexpr (c == 2) v = *reinterpret_cast<const uint32_t *>(rp + 16 * q);
+            else v = *reinterpret_cast<const uint64_t *>(rp + 16 * q);
+            word |= v << (q * B);
+        }
+        const uint32_t mb = (uint32_t)(Mb[(o * 32 + 32 - (32 >> c) + (o ? by : bx)) * 16 + (l0 >> 3)] >> (l0 & 7)) &
+                            ((1u << lpw) - 1);
+        uint64_t first;
+        if constexpr (c == 0) {
+            first = (uint64_t)(((mb >> 4) * 0x204081u) & 0x01010101u) << 32 | (((mb & 15u) * 0x204081u) & 0x01010101u);
+        } else if constexpr (c == 1) {
+            first = (uint64_t)(((mb >> 2) & 1u) | ((mb & 8u) << 13)) << 32 | ((mb & 1u) | ((mb & 2u) << 15));
+        } else if constexpr (c == 2) {
+            first = (uint64_t)(mb >> 1) << 32 | (mb & 1u);
+        } else {
+            first = mb;
+        }
+        word = (word & ~FM) | first;
+        // the next word of the block's scan (lane + 1), none after the block's last
+        uint32_t nx = 0;
+        if constexpr (G > 1) {
+            nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)word, 0x130, 0xF, 0xF, true);  // wave_shl 1
+            nx = j == G - 1 ? 0u : nx;
+        }
+        const uint64_t Z = ~word;
+        const uint64_t A = Z & ((word >> 1) | (uint64_t)(nx & 1u) << 63);
+        const uint64_t C = A & ((word >> 2) | (uint64_t)(nx & 3u) << 62);
+        uint32_t s = (uint32_t)(__popcll(Z) + __popcll(A) + 2 * __popcll(C));
+        uint32_t lz = Z ? j * 64 + 63 - (uint32_t)__builtin_clzll(Z) : 0u;  // the last zero bit (bit 0 is one)
+#pragma unroll
+        for (uint32_t st = 1; st < G; st <<= 1) {
+            const uint32_t s2 = shl_down(s, st), z2 = shl_down(lz, st);
+            s += s2;
+            lz = lz > z2 ? lz : z2;
+        }
+        uint32_t cost;
+        if (c >= 2 && ballot(Z == 0)) {  // a run may reach 259: the monoid (wave-uniform)
+            cost = seg_cost(seg_group(seg_leaf(word, 64), G, lane));
+        } else {
+            const uint32_t Lm = B * B - lz;  // the last run: run_cost(Lm - 1) + 1 for the counted g(Lm)
+            cost = s + (Lm >= 4 ? 1u : 0u) - (Lm == 3 ? 1u : 0u);
+        }
+        if (j == 0) hv[(o << (2 * lnb)) + (by << lnb) + bx] = cost;
+    }
+}
+
+// Whole tiles, B = 128 (one block per order): fast_cost's pattern count over the 256 words of
+// each order, one per thread (word j = half j & 1 of line j >> 1; the look-ahead reads the low
+// byte of word j + 1 itself, since it may sit in the next wave). Per wave and order: the count,
+// the last zero bit and whether a word is all ones, into st[o][wave] (the caller joins them).
+__device__ __forceinline__ void stats128(const uint64_t *E, const uint64_t *WM, uint32_t (*st)[4][3], uint32_t tid,
+                                         uint32_t lane, uint32_t wv)
+{
+    const uint8_t *Mb = reinterpret_cast<const uint8_t *>(WM);
+    const uint8_t *Eb = reinterpret_cast<const uint8_t *>(E);
+    auto wrap = [&](uint32_t o, uint32_t r) __attribute__((always_inline)) {
+        return (uint32_t)(Mb[(o * 32 + 30) * 16 + (r >> 3)] >> (r & 7)) & 1u;
+    };
+#pragma unroll
+    for (uint32_t o = 0; o < 2; ++o) {
+        const uint32_t j = tid;
+        uint64_t word = E[o * 2 * kTile + j];
+        if ((j & 1) == 0) word = (word & ~1ull) | wrap(o, j >> 1);
+        uint32_t nx = 0;
+        if (j < 2 * kTile - 1) {
+            nx = Eb[(o * 2 * kTile + j + 1) * 8];
+            if ((j & 1) == 1) nx = (nx & ~1u) | wrap(o, (j + 1) >> 1);
+        }
+        const uint64_t Z = ~word;
+        const uint64_t A = Z & ((word >> 1) | (uint64_t)(nx & 1u) << 63);
+        const uint64_t C = A & ((word >> 2) | (uint64_t)(nx & 3u) << 62);
+        const uint32_t s = (uint32_t)(__popcll(Z) + __popcll(A) + 2 * __popcll(C));
+        const uint32_t lz = Z ? j * 64 + 63 - (uint32_t)__builtin_clzll(Z) : 0u;
+        const uint32_t sw = readlane(wave_sum_incl(s), 63);
+        const uint32_t zw = readlane(wave_scan(lz, 0u, [](uint32_t x, uint32_t y) { return x > y ? x : y; }), 63);
+        const bool ones = ballot(Z == 0) != 0;
+        if (lane == 0) {
+            st[o][wv][0] = sw;
+            st[o][wv][1] = zw;
+            st[o][wv][2] = ones;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_cost_kernel(EncArgs a, Ws ws)
 {
     __shared__ uint8_t D[(kTile + 1) * kDS];  // DT(r, xl): y = ty0 + r - 1, x = tx0 + xl
     __shared__ uint64_t E[4 * kTile];         // Eh[r][2] then Ev[c][2]
-    __shared__ uint32_t hv[2][256];           // candidate's block costs, h / v
+    __shared__ uint32_t hv[2][2][256];        // candidate c's block costs, h / v: hv[c & 1]
     __shared__ Seg part[8];
-    __shared__ uint32_t red[4];
+    __shared__ uint64_t WM[2 * 32 * 2];       // wrap_masks (whole tiles)
+    __shared__ uint32_t st128[2][4][3];       // stats128
+    __shared__ uint32_t HV[682];              // whole tiles: every candidate's block costs (h then v)
+    __shared__ uint32_t edge[4 * kLU];        // tile_put
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[0];
     const bool diff = a.diff != 0;
@@ -664,7 +839,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
         AMeta &M = ws.meta[i];
         HC_TC_BEGIN();
         // 1. the tile plus one row above and one column to the left, diff model applied
-        if (g.ok) tile_put(D, g, v, diff, tid);
+        if (g.ok) tile_put(D, edge, g, v, diff, tid);
         if (t + gridDim.x < ntiles) {
             nx = tile_at(a, ws, t + gridDim.x);
             if (nx.ok) tile_fetch(nx, v, tid);
@@ -673,6 +848,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
         const uint64_t W = g.W, H = g.H, tx0 = g.tx0, ty0 = g.ty0;
         const uint64_t ntx = cdiv(W, kTile);
         const uint32_t tw = g.tw, th = g.th;
+        const bool whole = tw == kTile && th == kTile;
         HC_TC_MARK(1);
         // 2. Eh[r][k] bit j: x = tx0 + 64k + j equals x - 1 (row ty0 + r); Ev[c][k] bit j: y = ty0 +
         //    64k + j equals y - 1 (column tx0 + c). Eh: one word per thread from 16 dwords of its row
@@ -715,6 +891,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
             }
             const uint32_t c = 64 * (wv >> 1) + lane;  // lane L kept column 4 (16 (wv >> 1) + L / 4) + L % 4
             E[2 * kTile + 2 * c + kk] = c < tw ? keep : 0ull;
+            if (whole) wrap_masks(D, WM, wv, lane);
         }
         lds_barrier();
         const uint64_t *Eh = E, *Ev = E + 2 * kTile;
@@ -723,8 +900,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
         //    (one copy per candidate: B, the lines per word and the group sizes are constants, so
         //    each thread's LDS reads unroll and issue together)
         const uint32_t nct = M.nc < kTileCand ? M.nc : kTileCand;
+        uint32_t tot[kTileCand] = {};  // this thread's share of each candidate's total
         auto candidate = [&](auto cc) __attribute__((always_inline)) {
             constexpr uint32_t c = decltype(cc)::value;
+            uint32_t(*hx)[256] = hv[c & 1];  // double-buffered: one barrier per candidate
             constexpr uint32_t B = 8u << c, lg = 3 + c;
             const uint32_t nbx = (tw + B - 1) >> lg, nby = (th + B - 1) >> lg;
             const uint32_t per_o = (nbx * nby) << lg, items = 2 * per_o;
@@ -772,7 +951,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
                 const uint32_t G = 1u << lwpb;
                 sg = seg_group(sg, G < 64 ? G : 64u, lane);
                 if (G <= 64) {
-                    if ((lane & (G - 1)) == 0 && it < 2 * nwords) hv[o][blk] = seg_cost(sg);
+                    if ((lane & (G - 1)) == 0 && it < 2 * nwords) hx[o][blk] = seg_cost(sg);
                 } else if (lane == 0) {
                     part[4 * o + wv] = sg;
                 }
@@ -800,37 +979,89 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
                 }
                 s = seg_group(s, B < 64 ? B : 64u, lane);
                 if (B <= 64) {
-                    if ((lane & (B - 1)) == 0 && it < items) hv[o][blk] = seg_cost(s);
+                    if ((lane & (B - 1)) == 0 && it < items) hx[o][blk] = seg_cost(s);
                 } else if (lane == 0) {
                     part[wv] = s;
                 }
             }
             lds_barrier();
-            if (B == 128 && tid < 2)
-                hv[tid][0] = full ? seg_cost(seg_join(seg_join(part[4 * tid], part[4 * tid + 1]),
-                                                      seg_join(part[4 * tid + 2], part[4 * tid + 3])))
-                                  : seg_cost(seg_join(part[2 * tid], part[2 * tid + 1]));
-            lds_barrier();
+            if constexpr (B == 128) {
+                if (tid < 2)
+                    hx[tid][0] = full ? seg_cost(seg_join(seg_join(part[4 * tid], part[4 * tid + 1]),
+                                                          seg_join(part[4 * tid + 2], part[4 * tid + 3])))
+                                      : seg_cost(seg_join(part[2 * tid], part[2 * tid + 1]));
+                lds_barrier();
+            }
             // transform.cpp:113-123: the shorter scan, ties horizontal; word = cost | h << 31
             const uint32_t nblk = nbx * nby;
             const uint64_t per_row = cdiv(W, B);
             uint32_t sum = 0;
             for (uint32_t b = tid; b < nblk; b += 256) {
-                const uint32_t hc = hv[0][b], vc = hv[1][b];
+                const uint32_t hc = hx[0][b], vc = hx[1][b];
                 const uint64_t gi = (ty0 / B + b / nbx) * per_row + tx0 / B + b % nbx;
                 at<uint32_t>(ws, M.cost0[c])[gi] = hc <= vc ? (hc | 0x80000000u) : vc;
                 sum += hc <= vc ? hc : vc;
             }
-            for (uint32_t d = 32; d; d >>= 1) sum += __shfl_down(sum, d, 64);
-            if (lane == 0) red[wv] = sum;
-            lds_barrier();
-            if (tid == 0) atomicAdd(&M.total[c], (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
+            tot[c] += sum;
         };
-        if (nct > 0) candidate(std::integral_constant<uint32_t, 0>{});
-        if (nct > 1) candidate(std::integral_constant<uint32_t, 1>{});
-        if (nct > 2) candidate(std::integral_constant<uint32_t, 2>{});
-        if (nct > 3) candidate(std::integral_constant<uint32_t, 3>{});
-        if (nct > 4) candidate(std::integral_constant<uint32_t, 4>{});
+        if (whole && nct == kTileCand) {
+            // whole tiles: every candidate's block costs at once (one barrier), B = 128 from the
+            // per-wave counts unless a word is all ones
+            // (sched_barrier: one candidate's registers at a time; the prefetch holds 18)
+            fast_cost<0>(E, WM, HV, tid, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            fast_cost<1>(E, WM, HV + 512, tid, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            fast_cost<2>(E, WM, HV + 640, tid, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            fast_cost<3>(E, WM, HV + 672, tid, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            stats128(E, WM, st128, tid, lane, wv);
+            lds_barrier();
+            uint32_t ones = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) ones |= st128[k >> 2][k & 3][2];
+            // transform.cpp:113-123: the shorter scan, ties horizontal; word = cost | h << 31
+            auto put = [&](uint32_t c, uint32_t lnb, uint32_t off, uint32_t b, uint32_t hc, uint32_t vc)
+                __attribute__((always_inline)) {
+                    const uint32_t B = 8u << c;
+                    const uint64_t gi = (ty0 / B + (b >> lnb)) * cdiv(W, B) + tx0 / B + (b & ((1u << lnb) - 1));
+                    at<uint32_t>(ws, M.cost0[c])[gi] = hc <= vc ? (hc | 0x80000000u) : vc;
+                    tot[c] += hc <= vc ? hc : vc;
+                    (void)off;
+                };
+            put(0, 4, 0, tid, HV[tid], HV[256 + tid]);
+            if (tid < 64) {
+                put(1, 3, 512, tid, HV[512 + tid], HV[576 + tid]);
+            } else if (tid < 80) {
+                put(2, 2, 640, tid - 64, HV[640 + tid - 64], HV[656 + tid - 64]);
+            } else if (tid < 84) {
+                put(3, 1, 672, tid - 80, HV[672 + tid - 80], HV[676 + tid - 80]);
+            } else if (tid < 85 && !ones) {
+                uint32_t hv2[2];
+#pragma unroll
+                for (uint32_t o = 0; o < 2; ++o) {
+                    const uint32_t S = st128[o][0][0] + st128[o][1][0] + st128[o][2][0] + st128[o][3][0];
+                    const uint32_t z = max(max(st128[o][0][1], st128[o][1][1]), max(st128[o][2][1], st128[o][3][1]));
+                    const uint32_t Lm = kTile * kTile - z;
+                    hv2[o] = S + (Lm >= 4 ? 1u : 0u) - (Lm == 3 ? 1u : 0u);
+                }
+                put(4, 0, 680, 0, hv2[0], hv2[1]);
+            }
+            if (ones) candidate(std::integral_constant<uint32_t, 4>{});  // (uniform)
+        } else {
+            if (nct > 0) candidate(std::integral_constant<uint32_t, 0>{});
+            if (nct > 1) candidate(std::integral_constant<uint32_t, 1>{});
+            if (nct > 2) candidate(std::integral_constant<uint32_t, 2>{});
+            if (nct > 3) candidate(std::integral_constant<uint32_t, 3>{});
+            if (nct > 4) candidate(std::integral_constant<uint32_t, 4>{});
+        }
+        // the candidates' totals: one atomic per wave and candidate
+#pragma unroll
+        for (uint32_t c = 0; c < kTileCand; ++c) {
+            const uint32_t w = readlane(wave_sum_incl(tot[c]), 63);
+            if (lane == 0 && c < nct) atomicAdd(&M.total[c], (unsigned long long)w);
+        }
         HC_TC_MARK(3);
         // 4. tile summaries for the blocks of B >= 256
         if (M.nc > kTileCand) {
@@ -1697,10 +1928,13 @@ __global__ __launch_bounds__(64) void chunk_scan_kernel(DecArgs a, Ws ws)
     }
 }
 
-// one 16 KB chunk per workgroup, 64 bytes per thread held as 16 dwords: byte prefix sums inside
-// each dword (two shifted bytewise adds), carried along the thread's dwords, then across the
-// workgroup (a scan of the threads' totals) and from the chunks before (chunk_scan_kernel)
-__global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
+// one 16 KB chunk per workgroup as four 4 KB segments; in each, thread t holds 16 bytes at 16 t
+// (coalesced 16-byte loads and stores): byte prefix sums inside each dword (two shifted bytewise
+// adds), carried along the thread's 4 dwords; the four segments' thread totals packed one per
+// byte and scanned bytewise across the workgroup (mod 256 per byte, no carries between them);
+// the segments carried one after another from the chunks before (chunk_scan_kernel)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void undiff_kernel(DecArgs a, Ws ws)
 {
     __shared__ uint32_t part[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1709,38 +1943,86 @@ __global__ __launch_bounds__(256) void undiff_kernel(DecArgs a, Ws ws)
         const uint32_t i = find_item(ws.idx[1], a.n, t, ws.ctr[8 + 1]);
         const AMeta &M = ws.meta[i];
         const uint64_t c = t - ws.idx[1][i], n = M.w * M.h;
-        const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
-        uint8_t *mat = a.out + a.out_offs[i];
-        const uint64_t tb = b + 64ull * tid;
-        uint32_t w[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint64_t o = tb + 4 * k;
-            w[k] = o < e ? *reinterpret_cast<const uint32_t *>(mat + o) : 0u;
-            if (o < e && o + 4 > e) w[k] &= 0xFFFFFFFFu >> (8 * (o + 4 - e));
-        }
-        uint32_t run = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            uint32_t y = add8(w[k], w[k] << 8);
-            y = add8(y, y << 16);
-            w[k] = add8(y, run * 0x01010101u);
-            run = w[k] >> 24;
-        }
-        const uint32_t acc = wave_sum_incl(run);  // the threads' totals (mod 256)
-        if (lane == 63) part[wv] = acc;
-        lds_barrier();
-        uint32_t carry = at<uint8_t>(ws, M.csum)[c] + acc - run;
-        for (uint32_t k = 0; k < wv; ++k) carry += part[k];
-        carry = (carry & 0xFFu) * 0x01010101u;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint64_t o = tb + 4 * k;
-            const uint32_t v = add8(w[k], carry);
-            if (o + 4 <= e) *reinterpret_cast<uint32_t *>(mat + o) = v;
-            else
-                for (uint64_t q = o; q < e; ++q) mat[q] = (uint8_t)(v >> (8 * (q - o)));
-        }
+        const uint64_t b = c * kChunk, e64 = b + kChunk < n ? b + kChunk : n;
+        uint8_t *mat = a.out + a.out_offs[i] + b;  // this chunk
+        const uint32_t e = (uint32_t)(e64 - b);     // its length
+        auto run_chunk = [&](auto full) __attribute__((always_inline)) {
+            constexpr bool kFull = decltype(full)::value;
+            const uint32_t c0 = at<uint8_t>(ws, M.csum)[c];
+            uint32_t w[16];
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t o = 4096 * k + 16 * tid;
+                if (kFull || o + 16 <= e) {
+                    const u32x4 q = *reinterpret_cast<const u32x4 *>(mat + o);
+                    w[4 * k] = q.x;
+                    w[4 * k + 1] = q.y;
+                    w[4 * k + 2] = q.z;
+                    w[4 * k + 3] = q.w;
+                } else {
+    #pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        const uint32_t od = o + 4 * d;
+                        w[4 * k + d] = od < e ? *reinterpret_cast<const uint32_t *>(mat + od) : 0u;
+                        if (od < e && od + 4 > e) w[4 * k + d] &= 0xFFFFFFFFu >> (8 * (od + 4 - e));
+                    }
+                }
+            }
+            uint32_t tot = 0;  // byte k: this thread's total of segment k
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t run = 0;
+    #pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    uint32_t y = add8(w[4 * k + d], w[4 * k + d] << 8);
+                    y = add8(y, y << 16);
+                    w[4 * k + d] = add8(y, run * 0x01010101u);
+                    run = w[4 * k + d] >> 24;
+                }
+                tot |= run << (8 * k);
+            }
+            const uint32_t acc = wave_scan(tot, 0u, [](uint32_t x, uint32_t y) { return add8(x, y); });
+            if (lane == 63) part[wv] = acc;
+            lds_barrier();
+            uint32_t before = sub8(acc, tot);  // the threads before, per segment
+            uint32_t all = 0;                  // the segments' totals
+    #pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t pk = part[k];
+                if (k < wv) before = add8(before, pk);
+                all = add8(all, pk);
+            }
+            uint32_t seg = c0;  // carry into segment k: the chunks before + segments 0..k-1
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t add = ((seg + (before >> (8 * k))) & 0xFFu) * 0x01010101u;
+                seg += all >> (8 * k);
+                const uint32_t o = 4096 * k + 16 * tid;
+                u32x4 q;
+                q.x = add8(w[4 * k], add);
+                q.y = add8(w[4 * k + 1], add);
+                q.z = add8(w[4 * k + 2], add);
+                q.w = add8(w[4 * k + 3], add);
+                if (kFull || o + 16 <= e) {
+                    *reinterpret_cast<u32x4 *>(mat + o) = q;
+                } else {
+                    const uint32_t v4[4] = {q.x, q.y, q.z, q.w};
+    #pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        const uint32_t od = o + 4 * d;
+                        if (od + 4 <= e) {
+                            *reinterpret_cast<uint32_t *>(mat + od) = v4[d];
+                        } else if (od < e) {  // 1..3 bytes
+                            mat[od] = (uint8_t)v4[d];
+                            if (od + 1 < e) mat[od + 1] = (uint8_t)(v4[d] >> 8);
+                            if (od + 2 < e) mat[od + 2] = (uint8_t)(v4[d] >> 16);
+                        }
+                    }
+                }
+            }
+        };
+        if (e == kChunk) run_chunk(std::true_type{});
+        else run_chunk(std::false_type{});
         lds_barrier();
     }
 }

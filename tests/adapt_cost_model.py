@@ -82,6 +82,30 @@ def fold_bits(bits):
     return s
 
 
+def counted_cost(bits):
+    """tile_cost_kernel's fast path (fast_cost, whole 128 x 128 tiles, B <= 64): the scan's
+    64-bit words each count 1 + [L >= 2] + 2 [L >= 3] for every run starting in them (zeros,
+    zero-one, zero-one-one patterns with a two-bit look-ahead into the next word); the sum plus
+    the last run's rule (run_cost(L - 1) + 1 instead of the counted g(L), L from the last zero)
+    is the MNP-5 length while no run reaches 259 elements. None when a word is all ones in a scan
+    longer than 258 (B >= 32; the kernel folds the monoid for such a wave instead)."""
+    assert bits and bits[0] == 0
+    words = [sum(b << i for i, b in enumerate(bits[k:k + 64])) for k in range(0, len(bits), 64)]
+    ns = [min(64, len(bits) - k) for k in range(0, len(bits), 64)]
+    if len(bits) > 258 and any(w == (1 << n) - 1 for w, n in zip(words, ns)):
+        return None  # (B = 16: no run reaches 259; the last zero still ends the last run)
+    s = lz = 0
+    for j, (w, n) in enumerate(zip(words, ns)):
+        nx = words[j + 1] if j + 1 < len(words) else 0
+        z = ~w & ((1 << n) - 1)
+        a = z & ((w >> 1) | ((nx & 1) << (n - 1)))
+        c = a & ((w >> 2) | ((nx & 3) << (n - 2)))
+        s += popc(z) + popc(a) + 2 * popc(c)
+        lz = max(lz, j * 64 + z.bit_length() - 1)
+    Lm = len(bits) - lz
+    return s + (1 if Lm >= 4 else 0) - (1 if Lm == 3 else 0)
+
+
 def rle_len_via_bits(seq):
     return seg_cost(fold_bits(bits_of(seq)))
 

@@ -47,6 +47,23 @@ def test_seg_join_any_split():
         assert (j.n, j.lead, j.tail, j.mid) == (whole.n, whole.lead, whole.tail, whole.mid)
 
 
+def test_counted_cost(oracle_mod):
+    """the kernel's pattern-count cost for whole-tile blocks (B = 8..64: 64..4096 elements)
+    equals |applyRLE| whenever it applies (no all-ones word); runs of 1..300 elements"""
+    rng = random.Random(5)
+    used = 0
+    for k in range(600):
+        n = rng.choice([64, 256, 1024, 4096])
+        seq = _runs(rng, n, rng.choice([1, 3, 6, 40, 70, 300]), rng.choice([2, 3, 256]))
+        got = M.counted_cost(M.bits_of(seq))
+        if got is not None:
+            used += 1
+            assert got == len(oracle_mod.rle(bytes(seq))), (k, n)
+        else:
+            assert n > 258
+    assert used > 300
+
+
 def _matrix(kind, W, H, seed):
     rng = random.Random(seed)
     if kind == "flat":
