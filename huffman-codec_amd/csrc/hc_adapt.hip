@@ -1271,6 +1271,50 @@ __device__ __forceinline__ void emit_block(Value value, uint32_t L, uint8_t *out
     }
 }
 
+// popcount of m's bits below this lane (v_mbcnt)
+__device__ __forceinline__ uint32_t count_below(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// emit_block for a whole block of a tile image (L = B * B, a multiple of 64): no lane is past
+// the block, so only the last step has the last-element rules; element p = 64 s + lane sits at
+// LDS byte a(s) = a(0) + (s >> 1) dA + (s & 1) dB (B <= 64: dA = 2 dB, one step = 64 / B whole
+// lines; B = 128: half a line), so each step's read costs one add; positions from v_mbcnt.
+__device__ __forceinline__ void emit_whole(const uint8_t *D, uint32_t a0, uint32_t dA, uint32_t dB, uint32_t L,
+                                           uint8_t *out, uint32_t lane)
+{
+    const uint64_t lte = ~0ull >> (63 - lane);  // lanes at or below this one
+    uint32_t pv = 0, po = 0;  // value and run offset of the previous step's last element
+    uint64_t q = 0;           // bytes written
+    uint32_t addr = a0;
+    uint32_t v = D[addr];
+    for (uint32_t base = 0, s = 0; base < L; base += 64, ++s) {
+        const uint32_t p = base + lane;
+        const bool fin = base + 64 == L;  // (uniform)
+        addr += (s & 1) ? dA - dB : dB;
+        const uint32_t vn = D[addr];  // the next step's element (past the block on the last: unused)
+        const uint32_t prev = lane_shr1(v, pv);
+        const uint32_t nx = dpp<0x130>(v, readlane(vn, 0));  // wave_shl 1: the next element
+        const uint64_t sm = ballot(p == 0 || v != prev);
+        const uint64_t le = sm & lte;
+        const uint32_t o = le ? lane - (63u - (uint32_t)__builtin_clzll(le)) : po + 1 + lane;
+        const uint32_t j = o % 258u;
+        const bool last = fin && lane == 63;
+        const bool end = nx != v || (fin && lane == 62);
+        const uint32_t cnt = last ? 1u : (uint32_t)(j <= 2) + (uint32_t)(j == 257) + (uint32_t)(end && j >= 2 && j <= 256);
+        const uint64_t b1 = ballot(cnt >= 1), b2 = ballot(cnt == 2);
+        const uint64_t pos = q + count_below(b1) + count_below(b2);
+        const uint32_t first = (last || j <= 2) ? v : (j == 257 ? 255u : j - 2);
+        if (cnt >= 1) out[pos] = (uint8_t)first;
+        if (cnt == 2) out[pos + 1] = 0;
+        q += __popcll(b1) + __popcll(b2);
+        po = readlane(o, 63);
+        pv = readlane(v, 63);
+        v = vn;
+    }
+}
+
 // blocks of B <= 128: one workgroup per tile loads it once into LDS (as tile_cost_kernel
 // does), then each wave emits blocks of the tile from LDS
 __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
@@ -1324,7 +1368,23 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
                 return DT(yl + 1, xl);
             };
             const uint64_t off = readlane((uint32_t)lane_off, m) | (uint64_t)readlane((uint32_t)(lane_off >> 32), m) << 32;
-            emit_block(value, sx * sy, at<uint8_t>(ws, M.sym) + M.hdr + off, lane);
+            uint8_t *out = at<uint8_t>(ws, M.sym) + M.hdr + off;
+            if (sx == b32 && sy == b32) {  // (uniform) a whole block: B is a power of two
+                const uint32_t lg = (uint32_t)__builtin_ctz(b32);
+                const uint32_t lo = lane & (b32 - 1), hi = lane >> lg;  // element `lane`: line hi, offset lo
+                const uint32_t a0 = horiz ? (y0 + 1 + hi) * kDS + x0 + 4 + lo : (y0 + 1 + lo) * kDS + x0 + 4 + hi;
+                uint32_t dA, dB;
+                if (b32 <= 64) {
+                    dB = horiz ? (64u >> lg) * kDS : 64u >> lg;
+                    dA = 2 * dB;
+                } else {
+                    dA = horiz ? kDS : 1u;
+                    dB = horiz ? 64u : 64u * kDS;
+                }
+                emit_whole(D, a0, dA, dB, b32 * b32, out, lane);
+            } else {
+                emit_block(value, sx * sy, out, lane);
+            }
         }
         lds_barrier();
     }
@@ -1788,7 +1848,7 @@ struct SymRing {
 // transform.cpp:191-216 for blocks of B = 8..128 (mode 0): one workgroup per tile; each wave
 // reverts the blocks of one tile block row (one group: they follow each other in the stream)
 // into an LDS image of the tile, which then leaves as whole rows
-__global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void unblock_tile_kernel(DecArgs a, Ws ws)
 {
     __shared__ uint8_t T[kTile * kDS];
     __shared__ uint32_t ring[4][256];
@@ -1825,12 +1885,22 @@ __global__ __launch_bounds__(256) void unblock_tile_kernel(DecArgs a, Ws ws)
                 const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
                 const bool horiz = readlane(lane_h, bx) != 0;
                 const uint32_t inner = horiz ? sx : sy;
-                const float inv = 1.0f / (float)inner;
-                auto place = [&](uint64_t q, uint32_t v) {
-                    const uint32_t a1 = div_small((uint32_t)q, inner, inv), b1 = (uint32_t)q - a1 * inner;
-                    T[(y0 + (horiz ? a1 : b1)) * kDS + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
-                };
-                pos = revert_block(rd, pos, M.count, (uint64_t)sx * sy, place, lane);
+                if (sx == b32 && sy == b32) {  // (uniform) a whole block: shifts, B a power of two
+                    const uint32_t lg = (uint32_t)__builtin_ctz(b32);
+                    // element q -> line q >> lg, offset q & (B - 1): T byte base + line * sl + offset * so
+                    const uint32_t sl = horiz ? kDS : 1u, so = horiz ? 1u : kDS, tb = y0 * kDS + x0;
+                    auto place = [&](uint64_t q, uint32_t v) {
+                        T[tb + ((uint32_t)q >> lg) * sl + ((uint32_t)q & (b32 - 1)) * so] = (uint8_t)v;
+                    };
+                    pos = revert_block(rd, pos, M.count, (uint64_t)b32 * b32, place, lane);
+                } else {
+                    const float inv = 1.0f / (float)inner;
+                    auto place = [&](uint64_t q, uint32_t v) {
+                        const uint32_t a1 = div_small((uint32_t)q, inner, inv), b1 = (uint32_t)q - a1 * inner;
+                        T[(y0 + (horiz ? a1 : b1)) * kDS + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
+                    };
+                    pos = revert_block(rd, pos, M.count, (uint64_t)sx * sy, place, lane);
+                }
             }
         }
         lds_barrier();
@@ -1885,6 +1955,8 @@ __global__ __launch_bounds__(256) void unblock_kernel(DecArgs a, Ws ws)
 
 // transform.cpp:231-239 (prefix sum mod 256 over the linear matrix) in 16 KB chunks:
 // per-chunk byte sums, a per-stream scan of those, then the chunks' prefix sums
+// 16-byte vector of dwords at any 4-aligned address (diff revert loads / stores)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
 __global__ __launch_bounds__(256) void chunk_sum_kernel(DecArgs a, Ws ws)
 {
     __shared__ uint32_t red[4];
@@ -1895,12 +1967,24 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(DecArgs a, Ws ws)
         const AMeta &M = ws.meta[i];
         const uint64_t c = t - ws.idx[1][i], n = M.w * M.h;
         const uint64_t b = c * kChunk, e = b + kChunk < n ? b + kChunk : n;
-        const uint8_t *mat = a.out + a.out_offs[i];
+        const uint8_t *mat = a.out + a.out_offs[i] + b;  // this chunk (out_offs 4-aligned)
+        const uint32_t len = (uint32_t)(e - b);
         uint32_t s = 0;
-        for (uint64_t k = b + 4 * tid; k < e; k += 1024) {  // out_offs 4-aligned, chunks 16 KB
-            uint32_t w = *reinterpret_cast<const uint32_t *>(mat + k);
-            if (k + 4 > e) w &= 0xFFFFFFFFu >> (8 * (k + 4 - e));
-            s = __builtin_amdgcn_sad_u8(w, 0u, s);
+        if (len == kChunk) {  // 16-byte loads, 4 per thread
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const u32x4 q = *reinterpret_cast<const u32x4 *>(mat + 4096 * k + 16 * tid);
+                s = __builtin_amdgcn_sad_u8(q.x, 0u, s);
+                s = __builtin_amdgcn_sad_u8(q.y, 0u, s);
+                s = __builtin_amdgcn_sad_u8(q.z, 0u, s);
+                s = __builtin_amdgcn_sad_u8(q.w, 0u, s);
+            }
+        } else {
+            for (uint32_t k = 4 * tid; k < len; k += 1024) {
+                uint32_t w = *reinterpret_cast<const uint32_t *>(mat + k);
+                if (k + 4 > len) w &= 0xFFFFFFFFu >> (8 * (k + 4 - len));
+                s = __builtin_amdgcn_sad_u8(w, 0u, s);
+            }
         }
         for (uint32_t d = 32; d; d >>= 1) s += __shfl_down(s, d, 64);
         if ((tid & 63) == 0) red[tid >> 6] = s;
@@ -1933,7 +2017,6 @@ __global__ __launch_bounds__(64) void chunk_scan_kernel(DecArgs a, Ws ws)
 // adds), carried along the thread's 4 dwords; the four segments' thread totals packed one per
 // byte and scanned bytewise across the workgroup (mod 256 per byte, no carries between them);
 // the segments carried one after another from the chunks before (chunk_scan_kernel)
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void undiff_kernel(DecArgs a, Ws ws)
 {
     __shared__ uint32_t part[4];
