@@ -561,6 +561,25 @@ __device__ __forceinline__ void tile_fetch(const TileAt &g, uint32_t *v, uint32_
 {
     const uint32_t nd = (g.tw + 7) / 4, items = (g.th + 1) * nd;
     const bool aligned = ((reinterpret_cast<uintptr_t>(g.mat) | g.W) & 3) == 0;
+    if (aligned && g.ty0 > 0 && (g.ty0 + g.th - 1) * g.W + g.tx0 + 4 * nd - 4 <= g.n) {
+        // (uniform) every item inside the matrix: one pointer per thread, stepped q rows and
+        // rem dwords per item (one row more when the dword index wraps)
+        const uint32_t q = 256 / nd, rem = 256 - q * nd;
+        uint32_t d = tid % nd;
+        const uint8_t *p = g.mat + ((g.ty0 + tid / nd - 1) * g.W + g.tx0 - 4 + 4 * d);
+        const uint64_t step = q * g.W + 4 * rem, wrap = g.W - 4 * nd;
+#pragma unroll
+        for (uint32_t u = 0; u < kLU; ++u) {
+            v[u] = u * 256 + tid < items ? *reinterpret_cast<const uint32_t *>(p) : 0u;
+            d += rem;
+            p += step;
+            if (d >= nd) {
+                d -= nd;
+                p += wrap;
+            }
+        }
+        return;
+    }
     TileWalk wk(nd, tid);
 #pragma unroll
     for (uint32_t u = 0; u < kLU; ++u, wk.next()) {
@@ -592,10 +611,19 @@ __device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileA
             v[u] = sub8(v[u], (v[u] << 8) | (pv >> 24));
         }
     }
-    TileWalk wk(nd, tid);
+    // LDS byte kDS r + 4 d of item (r, d), stepped like tile_fetch's pointer
+    const uint32_t q = 256 / nd, rem = 256 - q * nd, step = q * kDS + 4 * rem, wrap = kDS - 4 * nd;
+    uint32_t d = tid % nd, at = (tid / nd) * kDS + 4 * d;
 #pragma unroll
-    for (uint32_t u = 0; u < kLU; ++u, wk.next())
-        if (u * 256 + tid < items) *reinterpret_cast<uint32_t *>(D + wk.r * kDS + 4 * wk.d) = v[u];
+    for (uint32_t u = 0; u < kLU; ++u) {
+        if (u * 256 + tid < items) *reinterpret_cast<uint32_t *>(D + at) = v[u];
+        d += rem;
+        at += step;
+        if (d >= nd) {
+            d -= nd;
+            at += wrap;
+        }
+    }
     lds_barrier();
 }
 

@@ -100,3 +100,43 @@ def test_adapt_batch_decode_errors_and_capacity(gpu, hc, oracle_mod, vectors):
     assert st == want
     st, _, lens = decompress_adapt_batch(hc, torch, [good], [len(r) - 1])
     assert st == [hc.HC_ERR_CAPACITY] and lens == [len(r)]
+
+
+def _scaled(B, W, H, seed, noise):
+    """constant B x B blocks of 3 values (the block size B wins), optionally with sparse noise
+    that cuts every run below 259 (whole tiles then take tile_cost's counted path throughout)"""
+    rng = np.random.default_rng(seed)
+    v = rng.integers(0, 3, size=((H + B - 1) // B, (W + B - 1) // B)).astype(np.uint8)
+    m = np.kron(v, np.ones((B, B), np.uint8))[:H, :W].copy()
+    if noise:
+        flat = m.reshape(-1)
+        idx = rng.integers(0, flat.size, size=flat.size // 40)
+        flat[idx] = rng.integers(0, 256, size=idx.size).astype(np.uint8)
+    return m.tobytes()
+
+
+@pytest.mark.parametrize("use_diff", [False, True])
+def test_adapt_whole_tiles_each_block_size(gpu, hc, oracle_mod, use_diff):
+    """whole 128 x 128 tiles where each candidate B = 8 .. 128 wins (blocks of that size), with
+    runs of thousands (the monoid fallbacks of the counted costs) and cut by noise (the counted
+    path): byte for byte the oracle, and the winning block sizes cover 8 .. 128"""
+    torch = gpu
+    raws, widths, won = [], [], set()
+    for B in (8, 16, 32, 64, 128):
+        for (W, H) in ((512, 512), (256, 384)):
+            for noise in (False, True):
+                pat = _scaled(B, W, H, B * 7 + W + noise, noise)
+                r = bytes(oracle_mod.undiff(pat)) if use_diff else pat  # the diff model sees pat
+                raws.append(r)
+                widths.append(W)
+                st = oracle_mod.adapt(pat, W, H)
+                st = st[1] if isinstance(st, tuple) else st
+                won.add(int.from_bytes(bytes(st[16:24]), "big"))
+    assert {8, 16, 32, 64, 128} <= won
+    st, enc, _ = compress_adapt_batch(hc, torch, raws, widths, use_diff)
+    assert st == [0] * len(raws)
+    for i, (r, w) in enumerate(zip(raws, widths)):
+        want_st, want = oracle_mod.compress(r, use_diff, True, w)
+        assert want_st == 0 and enc[i] == want, f"matrix {i}: GPU adaptive stream differs from the oracle"
+    dst, dec, _ = decompress_adapt_batch(hc, torch, enc, [len(r) for r in raws])
+    assert dst == [0] * len(raws) and dec == raws
