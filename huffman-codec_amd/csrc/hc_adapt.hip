@@ -1657,7 +1657,7 @@ __device__ __forceinline__ uint32_t block_size(const AMeta &m, uint64_t k, uint6
 #endif
 constexpr uint32_t kBW = HC_BOUNDS_W;   // symbol dwords per lane and step
 constexpr uint32_t kBStep = 256 * kBW;  // symbols per step
-__global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void bounds_kernel(DecArgs a, Ws ws)
 {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     for (uint32_t i = blockIdx.x * 4 + wv; i < a.n; i += gridDim.x * 4) {
@@ -1665,14 +1665,32 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
         if (M.status) continue;
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
         uint64_t *starts = at<uint64_t>(ws, M.starts);
-        const uint64_t per_row = cdiv(M.w, M.B), ntx = cdiv(M.w, kTile);
-        // the entry of block k (or ~0 if k starts no group)
-        auto entry = [&](uint64_t k) -> uint64_t {
-            if (M.mode == 0) {
-                const uint64_t bx = k % per_row;
-                return bx % M.K ? ~0ull : (k / per_row) * ntx + bx / M.K;
+        // the stream's parameters in registers (the starts[] stores could alias M's fields), and
+        // the current block's place stepped block by block (no 64-bit divisions per block)
+        const uint64_t W = M.w, H = M.h, B = M.B, K = M.K;
+        const bool tiled = M.mode == 0;
+        const uint64_t per_row = cdiv(W, B), ntx = cdiv(W, kTile);
+        uint64_t bx = 0, by = 0;   // block column / row of block blk
+        uint64_t kq = 0, gq = 0;   // mode 0: bx mod K, bx / K; else blk mod K, blk / K
+        auto block_want = [&]() -> uint64_t {
+            const uint64_t x0 = bx * B, y0 = by * B;
+            return (W - x0 < B ? W - x0 : B) * (H - y0 < B ? H - y0 : B);
+        };
+        // step to the next block; its group-start entry (~0 if it starts no group)
+        auto next_block = [&]() -> uint64_t {
+            if (++bx == per_row) {
+                bx = 0;
+                ++by;
+                if (tiled) kq = gq = 0;
+            } else if (tiled && ++kq == K) {
+                kq = 0;
+                ++gq;
             }
-            return k % M.K ? ~0ull : k / M.K;
+            if (!tiled && ++kq == K) {
+                kq = 0;
+                ++gq;
+            }
+            return kq ? ~0ull : (tiled ? by * ntx + gq : gq);
         };
         const uint64_t nsym = M.count, nb = M.nb;
         // the dwords behind symbols p + kBStep * ... of lane `lane` (the slab is 16-aligned and
@@ -1688,12 +1706,7 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
         uint32_t r = 0, last = 0;
         int status = 0;
         if (lane == 0 && nb) starts[0] = pos;
-        uint64_t want = 0;
-        if (nb) {
-            uint64_t x0, y0, sx, sy;
-            block_size(M, 0, &x0, &y0, &sx, &sy);
-            want = sx * sy;
-        }
+        uint64_t want = nb ? block_want() : 0;
         uint32_t cur[kBW + 1];
         load(pos, cur);
         while (blk < nb) {
@@ -1767,17 +1780,13 @@ __global__ __launch_bounds__(256) void bounds_kernel(DecArgs a, Ws ws)
                 }
                 lo = j + 1;
                 ++blk;
-                if (blk < nb && lane == 0) {
-                    const uint64_t e = entry(blk);
-                    if (e != ~0ull) starts[e] = pos + lo;
-                }
+                const uint64_t e = next_block();
+                if (blk < nb && lane == 0 && e != ~0ull) starts[e] = pos + lo;
                 if (blk == nb) {
                     pos += lo;
                     break;
                 }
-                uint64_t x0, y0, sx, sy;
-                block_size(M, blk, &x0, &y0, &sx, &sy);
-                want = sx * sy;
+                want = block_want();
                 got = 0;
                 r = 0;
                 if (lo == m) {

@@ -219,11 +219,14 @@ def test_adaptive_4096_digest(gpu, hc, digests):
         assert st == 0 and back == raw
 
 
-def test_roundtrip_property_full_batch(gpu, hc):
-    """size-independent property at the bench's per-GPU shape: decode(encode(x)) == x for a
-    1024-stream photo batch, and the encoded sizes are deterministic across two launches"""
+@pytest.mark.parametrize("n,use_diff", [(1024, True), (4096, False)], ids=["1024-cm", "C3-4096-c"])
+def test_roundtrip_property_full_batch(gpu, hc, digests, n, use_diff):
+    """size-independent properties at full batch shapes (1024 photo streams -c -m; config C3:
+    4096 streams -c, where the batch vote puts the encoder in table mode): decode(encode(x)) == x,
+    the encoded sizes are deterministic across two launches, and streams 0..3 (photo k = 0..3)
+    match the reference's digests"""
     torch = gpu
-    n, N = 1024, 262144
+    N = 262144
     raw = torch.empty(n * N, dtype=torch.uint8, device="cuda")
     hc.synth_batch("photo", 0, n, 512, 512, raw, N)
     offs = torch.arange(n, dtype=torch.int64, device="cuda") * N
@@ -234,9 +237,9 @@ def test_roundtrip_property_full_batch(gpu, hc):
     ecaps = torch.full((n,), cap, dtype=torch.int64, device="cuda")
     elens = torch.zeros(n, dtype=torch.int64, device="cuda")
     st = torch.zeros(n, dtype=torch.int32, device="cuda")
-    hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, st, use_diff=True)
+    hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, st, use_diff=use_diff)
     elens2 = torch.zeros_like(elens)
-    hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens2, st, use_diff=True)
+    hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens2, st, use_diff=use_diff)
     back = torch.empty_like(raw)
     blens = torch.zeros_like(lens)
     st2 = torch.zeros_like(st)
@@ -246,3 +249,8 @@ def test_roundtrip_property_full_batch(gpu, hc):
     assert torch.equal(elens, elens2)
     assert torch.equal(blens, lens)
     assert torch.equal(back, raw)
+    mode = "cm" if use_diff else "c"
+    for k in range(4):
+        e = enc[k * cap:k * cap + int(elens[k])].cpu().numpy().tobytes()
+        want = digests["synthetic"][f"photo_{k}"][mode]
+        assert (len(e), hashlib.sha256(e).hexdigest()) == (want["len"], want["sha256"]), (k, mode)
