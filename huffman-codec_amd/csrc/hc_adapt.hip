@@ -1305,27 +1305,34 @@ __device__ __forceinline__ uint32_t count_below(uint64_t m)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// emit_block for a whole block of a tile image (L = B * B, a multiple of 64): no lane is past
+// emit_block for whole blocks of a tile image (L = B * B, a multiple of 64): no lane is past
 // the block, so only the last step has the last-element rules; element p = 64 s + lane sits at
 // LDS byte a(s) = a(0) + (s >> 1) dA + (s & 1) dB (B <= 64: dA = 2 dB, one step = 64 / B whole
-// lines; B = 128: half a line), so each step's read costs one add; positions from v_mbcnt.
-__device__ __forceinline__ void emit_whole(const uint8_t *D, uint32_t a0, uint32_t dA, uint32_t dB, uint32_t L,
-                                           uint8_t *out, uint32_t lane)
-{
-    const uint64_t lte = ~0ull >> (63 - lane);  // lanes at or below this one
-    uint32_t pv = 0, po = 0;  // value and run offset of the previous step's last element
-    uint64_t q = 0;           // bytes written
-    uint32_t addr = a0;
-    uint32_t v = D[addr];
-    for (uint32_t base = 0, s = 0; base < L; base += 64, ++s) {
-        const uint32_t p = base + lane;
-        const bool fin = base + 64 == L;  // (uniform)
+// lines; B = 128: half a line), so each step's read costs one add; positions from v_mbcnt; the
+// previous value 0x100 before element 0 (no byte equals it) starts its run.
+struct EmitWhole {
+    uint32_t addr, dA, dB, pv, po, v;
+    uint64_t q;
+    uint8_t *out;
+    __device__ __forceinline__ void init(const uint8_t *D, uint32_t a0, uint32_t dA_, uint32_t dB_, uint8_t *o)
+    {
+        addr = a0;
+        dA = dA_;
+        dB = dB_;
+        pv = 0x100;  // differs from every byte: element 0 starts a run
+        po = 0;
+        q = 0;
+        out = o;
+        v = D[addr];
+    }
+    // step s (elements 64 s .. 64 s + 63); fin: the block's last step
+    __device__ __forceinline__ void step(const uint8_t *D, uint32_t s, bool fin, uint32_t lane, uint64_t lte)
+    {
         addr += (s & 1) ? dA - dB : dB;
         const uint32_t vn = D[addr];  // the next step's element (past the block on the last: unused)
         const uint32_t prev = lane_shr1(v, pv);
         const uint32_t nx = dpp<0x130>(v, readlane(vn, 0));  // wave_shl 1: the next element
-        const uint64_t sm = ballot(p == 0 || v != prev);
-        const uint64_t le = sm & lte;
+        const uint64_t le = ballot(v != prev) & lte;
         const uint32_t o = le ? lane - (63u - (uint32_t)__builtin_clzll(le)) : po + 1 + lane;
         const uint32_t j = o % 258u;
         const bool last = fin && lane == 63;
@@ -1340,6 +1347,22 @@ __device__ __forceinline__ void emit_whole(const uint8_t *D, uint32_t a0, uint32
         po = readlane(o, 63);
         pv = readlane(v, 63);
         v = vn;
+    }
+};
+
+// kN whole blocks of one size at once (independent chains, interleaved by the scheduler)
+template <int kN>
+__device__ __forceinline__ void emit_whole(const uint8_t *D, const uint32_t *a0, const uint32_t *dA,
+                                           const uint32_t *dB, uint32_t L, uint8_t *const *out, uint32_t lane)
+{
+    const uint64_t lte = ~0ull >> (63 - lane);  // lanes at or below this one
+    EmitWhole e[kN];
+#pragma unroll
+    for (int k = 0; k < kN; ++k) e[k].init(D, a0[k], dA[k], dB[k], out[k]);
+    for (uint32_t base = 0, s = 0; base < L; base += 64, ++s) {
+        const bool fin = base + 64 == L;  // (uniform)
+#pragma unroll
+        for (int k = 0; k < kN; ++k) e[k].step(D, s, fin, lane, lte);
     }
 }
 
@@ -1372,8 +1395,21 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
         const uint32_t nblk = nbx * nby;
         uint64_t lane_off = 0;
         uint32_t lane_h = 0;
-        for (uint32_t b = wv; b < nblk; b += 4) {
-            const uint32_t m = ((b - wv) >> 2) & 63;
+        // element `lane` of a whole block: line hi, offset lo; the address steps (emit_whole)
+        const uint32_t lg = (uint32_t)__builtin_ctz(b32);
+        const uint32_t lo = lane & (b32 - 1), hi = lane >> lg;
+        auto whole_at = [&](uint32_t b, bool horiz, uint32_t &a0, uint32_t &dA, uint32_t &dB) __attribute__((always_inline)) {
+            const uint32_t x0 = (b % nbx) * b32, y0 = (b / nbx) * b32;
+            a0 = horiz ? (y0 + 1 + hi) * kDS + x0 + 4 + lo : (y0 + 1 + lo) * kDS + x0 + 4 + hi;
+            if (b32 <= 64) {
+                dB = horiz ? (64u >> lg) * kDS : 64u >> lg;
+                dA = 2 * dB;
+            } else {
+                dA = horiz ? kDS : 1u;
+                dB = horiz ? 64u : 64u * kDS;
+            }
+        };
+        auto fetch = [&](uint32_t b, uint32_t m) __attribute__((always_inline)) {
             if (m == 0) {
                 const uint32_t bl = b + 4 * lane;
                 if (bl < nblk) {
@@ -1382,36 +1418,62 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
                     lane_h = (sym[24 + kl / 8] >> (7 - kl % 8)) & 1;
                 }
             }
-            const uint32_t bx = b % nbx, by = b / nbx;
-            const uint32_t x0 = bx * b32, y0 = by * b32;
-            const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
-            const bool horiz = readlane(lane_h, m) != 0;
-            const uint32_t inner = horiz ? sx : sy;
-            const float inv = 1.0f / (float)inner;
-            const bool pow2 = (inner & (inner - 1)) == 0;  // whole blocks: shifts, not a division
-            const uint32_t lgi = (uint32_t)__builtin_ctz(inner);
-            auto value = [&](uint32_t p) -> uint32_t {
-                const uint32_t a1 = pow2 ? p >> lgi : div_small(p, inner, inv), b1 = p - a1 * inner;
-                const uint32_t xl = x0 + (horiz ? b1 : a1), yl = y0 + (horiz ? a1 : b1);
-                return DT(yl + 1, xl);
-            };
+        };
+        auto out_of = [&](uint32_t m) __attribute__((always_inline)) {
             const uint64_t off = readlane((uint32_t)lane_off, m) | (uint64_t)readlane((uint32_t)(lane_off >> 32), m) << 32;
-            uint8_t *out = at<uint8_t>(ws, M.sym) + M.hdr + off;
-            if (sx == b32 && sy == b32) {  // (uniform) a whole block: B is a power of two
-                const uint32_t lg = (uint32_t)__builtin_ctz(b32);
-                const uint32_t lo = lane & (b32 - 1), hi = lane >> lg;  // element `lane`: line hi, offset lo
-                const uint32_t a0 = horiz ? (y0 + 1 + hi) * kDS + x0 + 4 + lo : (y0 + 1 + lo) * kDS + x0 + 4 + hi;
-                uint32_t dA, dB;
-                if (b32 <= 64) {
-                    dB = horiz ? (64u >> lg) * kDS : 64u >> lg;
-                    dA = 2 * dB;
-                } else {
-                    dA = horiz ? kDS : 1u;
-                    dB = horiz ? 64u : 64u * kDS;
+            return at<uint8_t>(ws, M.sym) + M.hdr + off;
+        };
+        if (tw % b32 == 0 && th % b32 == 0) {
+            // every block whole: up to four blocks of the wave at a time (b, b + 4, ...: fetch
+            // entries m .. m + 3, inside one 64-block fetch since m steps by 4 until the tail)
+            auto group = [&](auto nn, uint32_t b, uint32_t m) __attribute__((always_inline)) {
+                constexpr int kN = decltype(nn)::value;
+                uint32_t a0[kN], dA[kN], dB[kN];
+                uint8_t *out[kN];
+#pragma unroll
+                for (int k = 0; k < kN; ++k) {
+                    whole_at(b + 4 * k, readlane(lane_h, m + k) != 0, a0[k], dA[k], dB[k]);
+                    out[k] = out_of(m + k);
                 }
-                emit_whole(D, a0, dA, dB, b32 * b32, out, lane);
-            } else {
-                emit_block(value, sx * sy, out, lane);
+                emit_whole<kN>(D, a0, dA, dB, b32 * b32, out, lane);
+            };
+            for (uint32_t b = wv; b < nblk;) {
+                const uint32_t m = ((b - wv) >> 2) & 63;
+                fetch(b, m);
+                if (b + 12 < nblk) {
+                    group(std::integral_constant<int, 4>{}, b, m);
+                    b += 16;
+                } else if (b + 4 < nblk) {
+                    group(std::integral_constant<int, 2>{}, b, m);
+                    b += 8;
+                } else {
+                    group(std::integral_constant<int, 1>{}, b, m);
+                    b += 4;
+                }
+            }
+        } else {
+            for (uint32_t b = wv; b < nblk; b += 4) {
+                const uint32_t m = ((b - wv) >> 2) & 63;
+                fetch(b, m);
+                const uint32_t bx = b % nbx, by = b / nbx;
+                const uint32_t x0 = bx * b32, y0 = by * b32;
+                const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
+                const bool horiz = readlane(lane_h, m) != 0;
+                uint8_t *out = out_of(m);
+                if (sx == b32 && sy == b32) {  // (uniform) a whole block
+                    uint32_t a0, dA, dB;
+                    whole_at(b, horiz, a0, dA, dB);
+                    emit_whole<1>(D, &a0, &dA, &dB, b32 * b32, &out, lane);
+                } else {
+                    const uint32_t inner = horiz ? sx : sy;
+                    const float inv = 1.0f / (float)inner;
+                    auto value = [&](uint32_t p) -> uint32_t {
+                        const uint32_t a1 = div_small(p, inner, inv), b1 = p - a1 * inner;
+                        const uint32_t xl = x0 + (horiz ? b1 : a1), yl = y0 + (horiz ? a1 : b1);
+                        return DT(yl + 1, xl);
+                    };
+                    emit_block(value, sx * sy, out, lane);
+                }
             }
         }
         lds_barrier();
