@@ -1424,8 +1424,8 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
             return at<uint8_t>(ws, M.sym) + M.hdr + off;
         };
         if (tw % b32 == 0 && th % b32 == 0) {
-            // every block whole: up to four blocks of the wave at a time (b, b + 4, ...: fetch
-            // entries m .. m + 3, inside one 64-block fetch since m steps by 4 until the tail)
+            // every block whole: two blocks of the wave at a time (b, b + 4: fetch entries m, m + 1,
+            // inside one 64-block fetch since m steps by 2; four at a time measured slower: SGPRs)
             auto group = [&](auto nn, uint32_t b, uint32_t m) __attribute__((always_inline)) {
                 constexpr int kN = decltype(nn)::value;
                 uint32_t a0[kN], dA[kN], dB[kN];
@@ -1440,10 +1440,7 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
             for (uint32_t b = wv; b < nblk;) {
                 const uint32_t m = ((b - wv) >> 2) & 63;
                 fetch(b, m);
-                if (b + 12 < nblk) {
-                    group(std::integral_constant<int, 4>{}, b, m);
-                    b += 16;
-                } else if (b + 4 < nblk) {
+                if (b + 4 < nblk) {
                     group(std::integral_constant<int, 2>{}, b, m);
                     b += 8;
                 } else {
