@@ -1867,11 +1867,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void b
 // (block-relative index q in scan order, value) to place(); returns the block's end. A count
 // repeats the literal before it: literals are placed by their own lanes, each count's run
 // (up to 255 bytes) by the whole wave, 64 bytes at a time.
-template <class Read, class Place>
-__device__ __forceinline__ uint64_t revert_block(Read &&read, uint64_t pos, uint64_t count, uint64_t want,
+// Idx: the block-relative byte index type (uint32_t for the tile path's blocks of <= 2^14 bytes)
+template <class Idx = uint64_t, class Read, class Place>
+__device__ __forceinline__ uint64_t revert_block(Read &&read, uint64_t pos, uint64_t count, Idx want,
                                                  Place place, uint32_t lane)
 {
-    uint64_t got = 0;
+    Idx got = 0;
     uint32_t r = 0, last = 0;
     while (got < want && pos < count) {  // (the bounds pass proved the block whole)
         const uint32_t xs = read(pos);
@@ -1881,16 +1882,16 @@ __device__ __forceinline__ uint64_t revert_block(Read &&read, uint64_t pos, uint
         const uint32_t len = s == 3 ? xs : 1u;
         const uint32_t val = s == 3 ? pr : xs;
         const uint32_t acc = wave_sum_incl(len);
-        const uint64_t need = want - got;
-        const uint64_t hit = ballot((uint64_t)acc >= need);
+        const Idx need = want - got;
+        const uint64_t hit = ballot((Idx)acc >= need);
         const uint32_t L = hit ? (uint32_t)__builtin_ctzll(hit) : 63u;  // last lane of this block
         const bool mine = lane <= L;
-        const uint64_t q0 = got + acc - len;
+        const Idx q0 = got + acc - len;
         if (mine && len == 1) place(q0, val);
         for (uint64_t runs = ballot(mine && len > 1); runs; runs &= runs - 1) {
             const uint32_t l = (uint32_t)__builtin_ctzll(runs);
             const uint32_t n = readlane(len, l), v = readlane(val, l);
-            const uint64_t b = got + readlane(acc, l) - n;
+            const Idx b = got + readlane(acc, l) - n;
             for (uint32_t j0 = 0; j0 < n; j0 += 64)
                 if (j0 + lane < n) place(b + j0 + lane, v);
         }
@@ -1985,17 +1986,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void u
                     const uint32_t lg = (uint32_t)__builtin_ctz(b32);
                     // element q -> line q >> lg, offset q & (B - 1): T byte base + line * sl + offset * so
                     const uint32_t sl = horiz ? kDS : 1u, so = horiz ? 1u : kDS, tb = y0 * kDS + x0;
-                    auto place = [&](uint64_t q, uint32_t v) {
+                    auto place = [&](uint32_t q, uint32_t v) {
                         T[tb + ((uint32_t)q >> lg) * sl + ((uint32_t)q & (b32 - 1)) * so] = (uint8_t)v;
                     };
-                    pos = revert_block(rd, pos, M.count, (uint64_t)b32 * b32, place, lane);
+                    pos = revert_block<uint32_t>(rd, pos, M.count, b32 * b32, place, lane);
                 } else {
                     const float inv = 1.0f / (float)inner;
-                    auto place = [&](uint64_t q, uint32_t v) {
+                    auto place = [&](uint32_t q, uint32_t v) {
                         const uint32_t a1 = div_small((uint32_t)q, inner, inv), b1 = (uint32_t)q - a1 * inner;
                         T[(y0 + (horiz ? a1 : b1)) * kDS + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
                     };
-                    pos = revert_block(rd, pos, M.count, (uint64_t)sx * sy, place, lane);
+                    pos = revert_block<uint32_t>(rd, pos, M.count, sx * sy, place, lane);
                 }
             }
         }
