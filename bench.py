@@ -304,6 +304,46 @@ class AdaptBatch:
     encoded = Batch.encoded
 
 
+# algorithmic bytes of the adaptive stages that stream data (raw: matrix bytes, syms: adaptive
+# symbol bytes): what each must read and write at least
+ADAPT_STAGE_BYTES = {"tile_cost": lambda raw, syms: raw, "emit_tile": lambda raw, syms: raw + syms,
+                     "bounds": lambda raw, syms: syms, "unblock_tile": lambda raw, syms: syms + raw,
+                     "chunk_sum": lambda raw, syms: raw, "undiff": lambda raw, syms: 2 * raw}
+
+
+def adapt_stages(torch, hc, b, stream):
+    """one more encode + decode with the library's stage clock on (HIP events on the launch stream
+    after every stage): each stage's time, and for the streaming stages their algorithmic bytes
+    over that time against the HBM peak (8 TB/s)"""
+    hc.debug_stage_clock(True)
+    try:
+        hc.compress_adapt_batch(b.raw, b.offs, b.lens, b.widths, b.enc, b.eoffs, b.ecaps, b.elens, b.est,
+                                use_diff=b.use_diff, stream=stream, work=b.wenc)
+        enc = hc.debug_stage_times()
+        hc.decompress_adapt_batch(b.enc, b.eoffs, b.elens, b.back, b.offs, b.lens, b.blens, b.bst,
+                                  stream=stream, work=b.wdec)
+        dec = hc.debug_stage_times()
+    finally:
+        hc.debug_stage_clock(False)
+    torch.cuda.synchronize(b.dev)
+    raw = b.S * b.N
+    # adaptive symbols per stream: the FGK header's u64 count, the first 8 bytes of each stream
+    hdr = b.enc[b.eoffs.view(-1, 1) + torch.arange(8, device=b.dev)].to(torch.int64)
+    syms = int((hdr << (8 * torch.arange(8, device=b.dev))).sum())
+    out = {"adaptive_symbol_bytes": syms}
+    for direction, stages in (("encode", enc), ("decode", dec)):
+        d = {}
+        for name, ms in stages:
+            e = {"ms": round(ms, 4)}
+            if name in ADAPT_STAGE_BYTES and ms > 0:
+                nb = ADAPT_STAGE_BYTES[name](raw, syms)
+                gbs = nb / (ms * 1e-3) / 1e9
+                e.update({"alg_bytes": nb, "GBps": round(gbs, 1), "hbm_frac": round(gbs / 8000.0, 4)})
+            d[name] = e
+        out[direction] = d
+    return out
+
+
 def config_adapt(torch, hc, dev, stream, what, S, side, use_diff, steps, digests):
     """-c -a [-m] on S side x side photo matrices, device-resident, batched adaptive API; checked
     against the reference's digests (512x512 k = 0..3, or the 4096x4096 matrix) and by round trip"""
@@ -324,7 +364,7 @@ def config_adapt(torch, hc, dev, stream, what, S, side, use_diff, steps, digests
            "encode_GiBps": round(S * b.N / (enc_ms * 1e-3) / 2**30, 4),
            "decode_GiBps": round(S * b.N / (dec_ms * 1e-3) / 2**30, 4),
            "bits_per_byte": round(enc_bytes * 8 / (S * b.N), 4), "round_trip_exact": b.bad() == 0,
-           "reference_digests_identical": bool(ok)}
+           "reference_digests_identical": bool(ok), "stages": adapt_stages(torch, hc, b, stream)}
     del b
     torch.cuda.empty_cache()
     return out, bad

@@ -2247,18 +2247,57 @@ uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t
     return ws_header(n) + 8 * total_in + total_out / 4 + total_out / kChunk + 320ull * n + 4096;
 }
 
+// Diagnostic stage clock (hc_debug_stage_clock / hc_debug_stage_times, not in include/hcodec.h):
+// when on, the batched adaptive calls record a HIP event on their stream after every stage, so
+// a caller can read each stage's time of the last call (bench.py reports them per stage).
+struct StageClock {
+    bool on = false;
+    bool made = false;
+    int n = 0;
+    const char *name[32];
+    hipEvent_t ev[33];
+    void start(hipStream_t st)
+    {
+        n = 0;
+        if (!on) return;
+        if (!made) {
+            for (auto &e : ev)
+                if (hipEventCreate(&e) != hipSuccess) {
+                    on = false;
+                    return;
+                }
+            made = true;
+        }
+        (void)hipEventRecord(ev[0], st);
+    }
+    void mark(const char *nm, hipStream_t st)
+    {
+        if (!on || n >= 32) return;
+        name[n] = nm;
+        (void)hipEventRecord(ev[++n], st);
+    }
+};
+static StageClock g_clock;
+
 hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work, uint64_t work_bytes,
                               hipStream_t st)
 {
     if (b.n == 0) return hipSuccess;
     const Ws ws = carve(work, work_bytes, b.n);
     const EncArgs a{b.in, b.in_offs, b.in_lens, widths, b.n, (b.flags & HC_FLAG_DIFF) ? 1u : 0u};
+    g_clock.start(st);
     enc_plan_kernel<<<1, 1024, 0, st>>>(a, ws);
+    g_clock.mark("enc_plan", st);
     tile_cost_kernel<<<resident_grid(tile_cost_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("tile_cost", st);
     big_cost_kernel<<<resident_grid(big_cost_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("big_cost", st);
     choose_kernel<<<b.n < kGrid ? b.n : kGrid, 256, 0, st>>>(a, ws);
+    g_clock.mark("choose", st);
     emit_tile_kernel<<<resident_grid(emit_tile_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("emit_tile", st);
     emit_big_kernel<<<resident_grid(emit_big_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("emit_big", st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     Batch f = b;
@@ -2268,7 +2307,9 @@ hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work
     f.flags = (b.flags & HC_FLAG_DIFF) | HC_FLAG_ADAPT;
     e = launch_encode(f, SRC_SYMBOLS, st);
     if (e != hipSuccess) return e;
+    g_clock.mark("fgk_encode", st);
     status_fix_kernel<<<(b.n + 255) / 256, 256, 0, st>>>(ws, b.n, b.status, b.out_lens);
+    g_clock.mark("status_fix", st);
     return hipGetLastError();
 }
 
@@ -2277,7 +2318,9 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
     if (b.n == 0) return hipSuccess;
     const Ws ws = carve(work, work_bytes, b.n);
     const DecArgs a{b.in, b.in_offs, b.in_lens, b.n, b.out, b.out_offs, b.out_caps, b.out_lens, b.status};
+    g_clock.start(st);
     dec_plan_kernel<<<1, 1024, 0, st>>>(a, ws);
+    g_clock.mark("dec_plan", st);
     Batch f = b;
     f.in_lens = ws.lens2;
     f.out = ws.base;
@@ -2286,18 +2329,52 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
     f.out_lens = ws.sym_lens;
     hipError_t e = launch_decode(f, DST_SYMBOLS, st);
     if (e != hipSuccess) return e;
+    g_clock.mark("fgk_decode", st);
     dec_header_kernel<<<1, 1024, 0, st>>>(a, ws);
+    g_clock.mark("dec_header", st);
     bounds_kernel<<<resident_grid(bounds_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("bounds", st);
     unblock_tile_kernel<<<resident_grid(unblock_tile_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("unblock_tile", st);
     unblock_kernel<<<resident_grid(unblock_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("unblock", st);
     chunk_sum_kernel<<<resident_grid(chunk_sum_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("chunk_sum", st);
     chunk_scan_kernel<<<b.n < kGrid ? b.n : kGrid, 64, 0, st>>>(a, ws);
+    g_clock.mark("chunk_scan", st);
     undiff_kernel<<<resident_grid(undiff_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("undiff", st);
     dec_final_kernel<<<(b.n + 255) / 256, 256, 0, st>>>(a, ws);
+    g_clock.mark("dec_final", st);
     return hipGetLastError();
 }
 
 }  // namespace hc
+
+extern "C" int hc_debug_stage_clock(int on)
+{
+    hc::g_clock.on = on != 0;
+    hc::g_clock.n = 0;
+    return 0;
+}
+
+// the stages of the last batched adaptive call: names joined by '\n' into names (NUL-ended,
+// truncated to names_len), milliseconds into ms[0..max); returns the number of stages (waits for
+// the last one), or -1 if the clock is off or an event query fails
+extern "C" int hc_debug_stage_times(char *names, int names_len, float *ms, int max)
+{
+    hc::StageClock &c = hc::g_clock;
+    if (!c.on) return -1;
+    if (c.n && hipEventSynchronize(c.ev[c.n]) != hipSuccess) return -1;
+    int len = 0;
+    for (int k = 0; k < c.n && k < max; ++k) {
+        if (hipEventElapsedTime(&ms[k], c.ev[k], c.ev[k + 1]) != hipSuccess) return -1;
+        for (const char *p = c.name[k]; *p && len + 2 < names_len; ++p) names[len++] = *p;
+        if (len + 1 < names_len) names[len++] = '\n';
+    }
+    if (names_len > 0) names[len < names_len ? len : names_len - 1] = 0;
+    return c.n;
+}
 
 #ifdef HC_TC_PROF
 extern "C" int hc_debug_tc_prof(unsigned long long *out, int reset)

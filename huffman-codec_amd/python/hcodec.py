@@ -326,6 +326,26 @@ def debug_set_enc_tab(mode):
         raise HCodecError(f"hc_debug_set_enc_tab failed: {rc}")
 
 
+def debug_stage_clock(on):
+    """Diagnostic (not part of include/hcodec.h): when on, the batched adaptive calls record a
+    HIP event after each stage; debug_stage_times() reads the last call's stages."""
+    f = lib().hc_debug_stage_clock
+    f.argtypes = [ctypes.c_int]
+    f(1 if on else 0)
+
+
+def debug_stage_times():
+    """[(stage, ms), ...] of the last batched adaptive call (waits for it); needs the clock on"""
+    f = lib().hc_debug_stage_times
+    f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    names = ctypes.create_string_buffer(1024)
+    ms = (ctypes.c_float * 32)()
+    n = f(names, 1024, ms, 32)
+    if n < 0:
+        raise HCodecError("hc_debug_stage_times failed (clock off?)")
+    return list(zip(names.value.decode().split("\n")[:n], [float(ms[k]) for k in range(n)]))
+
+
 def compress_bound(n, use_adapt=False):
     return int(lib().hc_compress_bound(n, int(bool(use_adapt))))
 
