@@ -30,7 +30,7 @@ def main():
     for k in sorted(agg):
         c = {name: v / n[k] for name, v in agg[k].items()}
         waves = c.get("SQ_WAVES", 0) or 1
-        short = k.split("(")[0].replace("hc::(anonymous namespace)::", "")[:40]
+        short = k.replace("hc::(anonymous namespace)::", "").split("(")[0][:40]
         cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8
         fields = " ".join(f"{name.replace('SQ_', '').lower()}={v / waves:.0f}" for name, v in sorted(c.items())
                           if name not in ("SQ_WAVES", "GRBM_GUI_ACTIVE"))
