@@ -596,6 +596,8 @@ __device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileA
 {
     const uint32_t nd = (g.tw + 7) / 4, items = (g.th + 1) * nd;
     const uint32_t lane = tid & 63, wv = tid >> 6;
+    // the first barrier also ends the previous tile: no thread writes D before all have
+    // finished reading it (tile_cost_kernel has no barrier at the end of a tile)
     if (diff) {
         // the previous item's dword is lane - 1's (wave_shr 1); a wave's lane 0 takes it from the
         // lane 63 before it through edge[] (item u * 256 + tid - 1)
@@ -603,7 +605,9 @@ __device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileA
 #pragma unroll
             for (uint32_t u = 0; u < kLU; ++u) edge[4 * u + wv] = v[u];
         }
-        lds_barrier();
+    }
+    lds_barrier();
+    if (diff) {
 #pragma unroll
         for (uint32_t u = 0; u < kLU; ++u) {
             uint32_t pv = lane_shr1(v[u], 0u);
@@ -1112,8 +1116,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
                     piece_pack(s, (uint32_t)(w[0] & 1), DT(1, x), DT(th, x));
             }
         }
-        lds_barrier();
-        HC_TC_MARK(4);
+        HC_TC_MARK(4);  // (the next tile_put's first barrier ends this tile)
     }
 }
 

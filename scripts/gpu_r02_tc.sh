@@ -1,5 +1,10 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 300 python -u bench.py --only-configs A512,C4m > gpurun_out/stages.log 2>&1 || { echo "bench rc=$?"; tail -20 gpurun_out/stages.log; exit 1; }
-tail -1 gpurun_out/stages.log | cut -c1-300
+mkdir -p gpurun_out/prof
+rm -f gpurun_out/t44.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_adapt_batch.py tests/test_gpu_parity.py tests/test_gpu_huge.py -m gpu -x -q -rf --timeout 300 --timeout-method thread -k "adapt or digest" > gpurun_out/t44.log 2>&1 || { echo "tests failed rc=$?"; tail -30 gpurun_out/t44.log; exit 1; }
+tail -3 gpurun_out/t44.log
+for v in K J K J; do
+  HC_LIB_PATH=build_ab/$v/libhcodec.so timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof/tc$v -o tc -- python3 bench.py --only-configs A512 > gpurun_out/tc$v.log 2>&1 || exit 1
+  echo $v; python3 scripts/trace_summary.py gpurun_out/prof/tc$v/tc_kernel_trace.csv | grep -E "tile_cost"; rm -rf gpurun_out/prof/tc$v
+done
