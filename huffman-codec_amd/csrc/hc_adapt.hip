@@ -845,6 +845,12 @@ __device__ __forceinline__ void stats128(const uint64_t *E, const uint64_t *WM, 
     }
 }
 
+// transform.cpp:97-134 / 294-328 (every candidate block's h / v scan length) for B <= 128, one
+// workgroup per 128 x 128 tile of the work list (persistent grid): 1. the tile image in LDS
+// (tile_put; the next tile's loads in flight meanwhile), 2. the Eh / Ev equality words (and the
+// wrap masks of a whole tile), 3. every candidate's block costs (fast_cost / stats128 on whole
+// tiles, the run-segment monoid on partial ones) into the cost words and per-candidate totals,
+// 4. the tile row / column summaries the blocks of B >= 256 are joined from (big_cost_kernel).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_cost_kernel(EncArgs a, Ws ws)
 {
     __shared__ uint8_t D[(kTile + 1) * kDS];  // DT(r, xl): y = ty0 + r - 1, x = tx0 + xl
