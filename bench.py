@@ -399,6 +399,25 @@ def run_configs(torch, hc, dev, stream, only):
     return res, bad
 
 
+def copy_peak(torch, dev, stream, nbytes=1 << 30, reps=5):
+    """measured HBM reference point next to the 8 TB/s datasheet peak: a 1 GiB
+    device-to-device tensor copy, (read + write bytes) / best time, GB/s"""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    best = None
+    with torch.cuda.stream(stream):
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            dst.copy_(src)
+            e1.record(stream)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+    del src, dst
+    return round(2 * nbytes / (best * 1e-3) / 1e9, 1)
+
+
 def time_gather(torch, hcdist, b, dev, barrier):
     """every rank's encoded streams packed back to back on its GPU (hc_pack_batch), then sent to
     rank 0 point to point; max over ranks of the wall time; rank 0 checks the bytes it got"""
@@ -485,6 +504,8 @@ def main():
         "decode_GiBps": round(world * S * N_RAW / (dec_ms * 1e-3) / 2**30, 4),
         "bits_per_byte": round(enc_total * 8 / raw_total, 4), "bit_exact": True,
     }
+    if world == 1:
+        roof["measured_copy_GBps"] = copy_peak(torch, dev, stream)
     if args.gather:
         result["gather"] = time_gather(torch, hcdist, b, dev, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
