@@ -85,3 +85,28 @@ def test_bounds_many_blocks_per_step(gpu, hc, oracle_mod):
     want_st, want = oracle_mod.decompress(data)
     st, got = hc.decompress(data)
     assert want_st == 0 and st == 0 and got == want
+
+
+def test_bounds_other_block_sizes_vs_oracle(gpu, hc, oracle_mod):
+    """block sizes a forged header may carry besides 8..128: B >= 256 (one start entry per
+    block) and sizes that are not powers of two (K-block groups, K > 1 for small blocks), ragged
+    matrices with several block rows and groups; valid, starved and overlong streams"""
+    rng = np.random.default_rng(99)
+    seen = set()
+    cases = [(300, 270, 256), (530, 260, 256), (520, 300, 512), (100, 90, 3), (77, 41, 5), (130, 70, 12),
+             (200, 150, 24), (333, 121, 40), (250, 260, 100), (610, 300, 300), (64, 64, 7), (90, 200, 9)]
+    for case, (w, h, b) in enumerate(cases):
+        hdr, body = adaptive_stream(rng, w, h, b)
+        kind = case % 3
+        if kind == 1:
+            body = body[: max(0, len(body) - int(rng.integers(1, 6)))]
+        elif kind == 2:
+            body = body + [int(v) for v in rng.integers(0, 4, size=int(rng.integers(1, 4)))]
+        data = container(oracle_mod, hdr + body)
+        want_st, want = oracle_mod.decompress(data)
+        st, got = hc.decompress(data)
+        assert st == want_st, (case, w, h, b, kind)
+        if st == 0:
+            assert got == want, (case, w, h, b)
+        seen.add(st)
+    assert 0 in seen and len(seen) >= 2, seen
