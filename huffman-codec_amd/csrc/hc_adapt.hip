@@ -2267,8 +2267,8 @@ struct StageClock {
     hipEvent_t ev[33];
     void start(hipStream_t st)
     {
+        if (!on) return;  // (off: no shared state touched, calls stay re-entrant)
         n = 0;
-        if (!on) return;
         if (!made) {
             for (auto &e : ev)
                 if (hipEventCreate(&e) != hipSuccess) {
