@@ -12,6 +12,8 @@
 #include <string.h>
 
 #include <hipcub/hipcub.hpp>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "hc_internal.h"
@@ -25,6 +27,25 @@ namespace {
 
 constexpr uint64_t kAlign = 16;
 uint64_t up16(uint64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// copy(k) for k in [0, n) on up to 8 host threads when the bytes are many (staging into and out
+// of pinned memory: one thread's memcpy would hold back the PCIe copies and the kernels)
+template <class Copy>
+void par_copy(uint32_t n, uint64_t bytes, Copy copy)
+{
+    const uint32_t hw = std::thread::hardware_concurrency();
+    const uint32_t t = bytes < (32ull << 20) || n < 2 ? 1u : (hw < 2 ? 1u : (hw < 8 ? hw : 8u));
+    if (t == 1) {
+        for (uint32_t k = 0; k < n; ++k) copy(k);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint32_t w = 0; w < t; ++w)
+        th.emplace_back([&, w] {
+            for (uint32_t k = (uint32_t)((uint64_t)n * w / t); k < (uint32_t)((uint64_t)n * (w + 1) / t); ++k) copy(k);
+        });
+    for (auto &x : th) x.join();
+}
 
 // length of the produced bytes that travel back (failed streams: none)
 __global__ void kept_lengths(const uint64_t *lens, const int32_t *status, uint64_t *kept, uint32_t n)
@@ -113,6 +134,11 @@ struct Slot {
     }
 };
 
+struct Pool {
+    std::mutex mu;
+    Slot slots[2];
+};
+
 struct Job {
     bool encode;
     bool adapt;              // -a streams: the batched adaptive device API (widths: encode only)
@@ -173,7 +199,6 @@ int launch(Job &j, Slot &s)
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t i = s.first + k;
         const uint64_t len = j.in_lens[i];
-        if (len) memcpy(s.hin.p + io, j.in[i], len);
         up[k] = io;
         up[n + k] = len;
         up[2 * n + k] = oo;
@@ -182,6 +207,9 @@ int launch(Job &j, Slot &s)
         io += up16(len);
         oo += up16(j.dcap[i]);
     }
+    par_copy(n, in_bytes, [&](uint32_t k) {
+        if (up[n + k]) memcpy(s.hin.p + up[k], j.in[s.first + k], up[n + k]);
+    });
     PIPE_CK(hipMemcpyAsync(s.din.p, s.hin.p, in_bytes, hipMemcpyHostToDevice, s.st));
     PIPE_CK(hipMemcpyAsync(s.dup.p, up, cols * n * sizeof(uint64_t), hipMemcpyHostToDevice, s.st));
     const uint64_t *d = s.dup.p;
@@ -230,12 +258,14 @@ int finish(Job &j, Slot &s, std::vector<uint32_t> &redo)
         PIPE_CK(hipMemcpyAsync(s.hpacked.p, s.dpacked.p, total, hipMemcpyDeviceToHost, s.st));
         PIPE_CK(hipStreamSynchronize(s.st));
     }
+    par_copy(n, total, [&](uint32_t k) {
+        if (st[k] == 0 && lens[k]) memcpy(j.out[s.first + k], s.hpacked.p + at[k], lens[k]);
+    });
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t i = s.first + k;
         j.out_lens[i] = lens[k];
         j.status[i] = st[k];
         if (st[k] == 0) {
-            if (lens[k]) memcpy(j.out[i], s.hpacked.p + at[k], lens[k]);
         } else if (st[k] == HC_ERR_CAPACITY && j.dcap[i] < j.out_caps[i]) {
             // the guess was short: code it again with what it needs (or all the caller has)
             j.dcap[i] = lens[k] < j.out_caps[i] ? lens[k] : j.out_caps[i];
@@ -266,10 +296,18 @@ int run(Job &j, uint32_t n)
     const uint64_t max_streams = env_u64("HC_PIPE_STREAMS", 8192);
     j.dcap.resize(n);
     for (uint32_t i = 0; i < n; ++i) j.dcap[i] = guess_cap(j, i);
-    Slot slots[2];
-    for (Slot &s : slots) {
-        PIPE_CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
-        PIPE_CK(hipEventCreateWithFlags(&s.meta_done, hipEventDisableTiming));
+    // the two slots and their pinned / device buffers persist between calls (allocating and
+    // pinning a GiB per call cost more than the coding); a concurrent call gets its own
+    static Pool *const pool = new Pool;  // never freed: the HIP runtime may be gone at exit
+    std::unique_lock<std::mutex> lk(pool->mu, std::try_to_lock);
+    Slot local[2];
+    Slot *const slots = lk.owns_lock() ? pool->slots : local;
+    for (int k = 0; k < 2; ++k) {
+        Slot &s = slots[k];
+        s.busy = false;
+        if (!s.st) PIPE_CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+        if (!s.meta_done) PIPE_CK(hipEventCreateWithFlags(&s.meta_done, hipEventDisableTiming));
+        PIPE_CK(hipStreamSynchronize(s.st));  // (a call that failed may have left work queued)
     }
     std::vector<uint32_t> order(n), redo;
     for (uint32_t i = 0; i < n; ++i) order[i] = i;
