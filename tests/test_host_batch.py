@@ -35,6 +35,36 @@ def test_host_batch_roundtrip_vs_oracle(gpu, hc, oracle_mod, use_diff, slots, mo
 
 
 @pytest.mark.gpu
+def test_host_batch_concurrent_calls(gpu, hc, oracle_mod):
+    """calls from several host threads at once (ctypes drops the GIL): one takes the persistent
+    pipeline slots, the others their own; every result byte-identical to the oracle, and a
+    second round reuses the slots"""
+    import threading
+    sets = [[oracle_mod.synth(kind, k, 128, 96).tobytes() for k in range(6)] for kind in ("photo", "grad", "noise")]
+    want = [[oracle_mod.compress(r, True, False, 512)[1] for r in raws] for raws in sets]
+    for _ in range(2):
+        got, errs = [None] * len(sets), []
+
+        def work(i):
+            try:
+                st, enc, _ = hc.compress_host_batch(sets[i], use_diff=True)
+                dst, dec, _ = hc.decompress_host_batch(enc, [len(r) for r in sets[i]])
+                got[i] = (st, enc, dst, dec)
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=work, args=(i,)) for i in range(len(sets))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        for i, (st, enc, dst, dec) in enumerate(got):
+            assert st == [0] * len(sets[i]) and enc == want[i]
+            assert dst == [0] * len(sets[i]) and dec == sets[i]
+
+
+@pytest.mark.gpu
 def test_host_batch_statuses(gpu, hc, oracle_mod):
     raw = oracle_mod.synth("photo", 2, 64, 64).tobytes()
     _, want = oracle_mod.compress(raw, True, False, 512)
