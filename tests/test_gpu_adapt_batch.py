@@ -140,3 +140,26 @@ def test_adapt_whole_tiles_each_block_size(gpu, hc, oracle_mod, use_diff):
         assert want_st == 0 and enc[i] == want, f"matrix {i}: GPU adaptive stream differs from the oracle"
     dst, dec, _ = decompress_adapt_batch(hc, torch, enc, [len(r) for r in raws])
     assert dst == [0] * len(raws) and dec == raws
+
+
+def test_stage_clock(gpu, hc, oracle_mod):
+    """the diagnostic stage clock bench.py reads: every stage of both batched adaptive calls,
+    in launch order, with non-negative times; off again afterwards (the calls unchanged)"""
+    torch = gpu
+    raws = [oracle_mod.synth("photo", k, 256, 256).tobytes() for k in range(4)]
+    hc.debug_stage_clock(True)
+    try:
+        st, enc, _ = compress_adapt_batch(hc, torch, raws, [256] * 4, True)
+        enc_stages = hc.debug_stage_times()
+        dst, dec, _ = decompress_adapt_batch(hc, torch, enc, [len(r) for r in raws])
+        dec_stages = hc.debug_stage_times()
+    finally:
+        hc.debug_stage_clock(False)
+    assert st == [0] * 4 and dst == [0] * 4 and dec == raws
+    assert [n for n, _ in enc_stages] == ["enc_plan", "tile_cost", "big_cost", "choose", "emit_tile", "emit_big",
+                                         "fgk_encode", "status_fix"]
+    assert [n for n, _ in dec_stages] == ["dec_plan", "fgk_decode", "dec_header", "bounds", "unblock_tile",
+                                         "unblock", "chunk_sum", "chunk_scan", "undiff", "dec_final"]
+    assert all(ms >= 0 for _, ms in enc_stages + dec_stages)
+    with pytest.raises(hc.HCodecError):
+        hc.debug_stage_times()
