@@ -315,6 +315,7 @@ def adapt_stages(torch, hc, b, stream):
     """one more encode + decode with the library's stage clock on (HIP events on the launch stream
     after every stage): each stage's time, and for the streaming stages their algorithmic bytes
     over that time against the HBM peak (8 TB/s)"""
+    hc.use_debug_build(True)  # the stage clock exists in the debug build only
     hc.debug_stage_clock(True)
     try:
         hc.compress_adapt_batch(b.raw, b.offs, b.lens, b.widths, b.enc, b.eoffs, b.ecaps, b.elens, b.est,
@@ -325,6 +326,7 @@ def adapt_stages(torch, hc, b, stream):
         dec = hc.debug_stage_times()
     finally:
         hc.debug_stage_clock(False)
+        hc.use_debug_build(False)
     torch.cuda.synchronize(b.dev)
     raw = b.S * b.N
     # adaptive symbols per stream: the FGK header's u64 count, the first 8 bytes of each stream

@@ -86,6 +86,7 @@ struct AMeta {
                                      // per block (B >= 256, power of 2), 2 K-block groups (other B)
     uint32_t pad2;
     uint64_t tiles;                  // decode: tiles (mode 0)
+    uint64_t ents;                   // decode: group-start entries reserved at `starts`
 };
 
 // workspace: [meta n][idx0 n+1][idx1 n+1][idx2 n+1][idx3 n+1][sym_offs n][sym_lens n][sym_caps n]
@@ -1656,6 +1657,22 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
             m.K = area >= kGroupBytes ? 1 : cdiv(kGroupBytes, area ? area : 1);
             m.groups = cdiv(nb, m.K);
         }
+        // the group-start entries the bounds pass writes must fit the ones reserved for this
+        // stream (dec_plan: group_entries_bound of the output capacity). Genuine streams always
+        // do (W, H >= 8); a forged header with a matrix 1..7 wide or high can name more tile
+        // block rows than that, and takes K-block groups large enough to fit instead
+        const uint64_t room = group_entries_bound(a.out_caps[i]);
+        const uint64_t ents = m.mode == 0 ? cdiv(h, b) * cdiv(w, kTile) : m.groups;
+        if (ents > room) {
+            const uint64_t bx = b < w ? b : w, by = b < h ? b : h, area = bx * by;
+            uint64_t K = area >= kGroupBytes ? 1 : cdiv(kGroupBytes, area ? area : 1);
+            if (cdiv(nb, K) > room) K = cdiv(nb, room);
+            m.mode = 2;
+            m.K = K;
+            m.groups = cdiv(nb, K);
+            m.tiles = 0;
+        }
+        m.ents = m.mode == 0 ? cdiv(h, b) * cdiv(w, kTile) : m.groups;
         m.chunks = m.diff ? cdiv(w * h, kChunk) : 0;
     };
     for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) parse(i);
@@ -1735,7 +1752,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void b
         uint64_t *starts = at<uint64_t>(ws, M.starts);
         // the stream's parameters in registers (the starts[] stores could alias M's fields), and
         // the current block's place stepped block by block (no 64-bit divisions per block)
-        const uint64_t W = M.w, H = M.h, B = M.B, K = M.K;
+        const uint64_t W = M.w, H = M.h, B = M.B, K = M.K, ents = M.ents;
         const bool tiled = M.mode == 0;
         const uint64_t per_row = cdiv(W, B), ntx = cdiv(W, kTile);
         uint64_t bx = 0, by = 0;   // block column / row of block blk
@@ -1849,7 +1866,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void b
                 lo = j + 1;
                 ++blk;
                 const uint64_t e = next_block();
-                if (blk < nb && lane == 0 && e != ~0ull) starts[e] = pos + lo;
+                if (blk < nb && lane == 0 && e < ents) starts[e] = pos + lo;  // (e = ~0: no group start)
                 if (blk == nb) {
                     pos += lo;
                     break;
@@ -2256,9 +2273,11 @@ uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t
     return ws_header(n) + 8 * total_in + total_out / 4 + total_out / kChunk + 320ull * n + 4096;
 }
 
-// Diagnostic stage clock (hc_debug_stage_clock / hc_debug_stage_times, not in include/hcodec.h):
-// when on, the batched adaptive calls record a HIP event on their stream after every stage, so
-// a caller can read each stage's time of the last call (bench.py reports them per stage).
+// Diagnostic stage clock (debug build only, hc_debug_stage_clock / hc_debug_stage_times): when
+// on, the batched adaptive calls record a HIP event on their stream after every stage, so a
+// caller can read each stage's time of its thread's last call (bench.py reports them per stage).
+// Per thread: concurrent calls from several threads keep separate clocks.
+#ifdef HC_DEBUG_HOOKS
 struct StageClock {
     bool on = false;
     bool made = false;
@@ -2267,7 +2286,7 @@ struct StageClock {
     hipEvent_t ev[33];
     void start(hipStream_t st)
     {
-        if (!on) return;  // (off: no shared state touched, calls stay re-entrant)
+        if (!on) return;
         n = 0;
         if (!made) {
             for (auto &e : ev)
@@ -2286,7 +2305,14 @@ struct StageClock {
         (void)hipEventRecord(ev[++n], st);
     }
 };
-static StageClock g_clock;
+static thread_local StageClock g_clock;
+#else
+struct StageClock {  // the shipping build: no clock, nothing recorded
+    void start(hipStream_t) const {}
+    void mark(const char *, hipStream_t) const {}
+};
+static constexpr StageClock g_clock{};
+#endif
 
 hipError_t adapt_encode_batch(const Batch &b, const uint64_t *widths, void *work, uint64_t work_bytes,
                               hipStream_t st)
@@ -2360,6 +2386,7 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
 
 }  // namespace hc
 
+#ifdef HC_DEBUG_HOOKS
 extern "C" int hc_debug_stage_clock(int on)
 {
     hc::g_clock.on = on != 0;
@@ -2384,6 +2411,8 @@ extern "C" int hc_debug_stage_times(char *names, int names_len, float *ms, int m
     if (names_len > 0) names[len < names_len ? len : names_len - 1] = 0;
     return c.n;
 }
+
+#endif  // HC_DEBUG_HOOKS
 
 #ifdef HC_TC_PROF
 extern "C" int hc_debug_tc_prof(unsigned long long *out, int reset)

@@ -8,6 +8,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "hc_internal.h"
@@ -16,13 +19,76 @@ namespace {
 
 using hc::Batch;
 
+// Device scratch of the single-buffer API. A call takes buffers from a per-device free list
+// (hipMalloc only when none is large enough) and gives them back at its end, so a process that
+// codes file after file (the CLI, C2) stops allocating after its first call. The list keeps at
+// most kKeepBytes per device (larger leftovers are freed at once) and hc_release_cached() frees
+// it. It caches memory only: no result depends on it, and concurrent calls never share a buffer.
+constexpr uint64_t kKeepBytes = 1ull << 30;
+struct FreeList {
+    std::mutex mu;
+    std::vector<std::pair<void *, uint64_t>> bufs[64];  // per device: (pointer, bytes)
+    uint64_t kept[64] = {};
+};
+FreeList &free_list()
+{
+    static FreeList *const f = new FreeList;  // never destroyed: the HIP runtime may be gone at exit
+    return *f;
+}
+
 struct DevBuf {
     void *p = nullptr;
-    ~DevBuf()
+    uint64_t cap = 0;
+    int dev = -1;
+    ~DevBuf() { give_back(); }
+    void give_back()
     {
+        if (!p) return;
+        FreeList &f = free_list();
+        {
+            std::lock_guard<std::mutex> lk(f.mu);
+            if (dev >= 0 && dev < 64 && f.kept[dev] + cap <= kKeepBytes) {
+                f.bufs[dev].emplace_back(p, cap);
+                f.kept[dev] += cap;
+                p = nullptr;
+            }
+        }
         if (p) (void)hipFree(p);
+        p = nullptr;
     }
-    hipError_t alloc(size_t n) { return hipMalloc(&p, n ? n : 16); }
+    // at least n bytes: the smallest cached buffer that fits, else a new one (one retry after
+    // freeing the cache when the device is short of memory)
+    hipError_t alloc(uint64_t n)
+    {
+        give_back();
+        n = n < 16 ? 16 : (n + 255) & ~255ull;
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+        if (dev >= 0 && dev < 64) {
+            FreeList &f = free_list();
+            std::lock_guard<std::mutex> lk(f.mu);
+            auto &v = f.bufs[dev];
+            size_t best = v.size();
+            for (size_t k = 0; k < v.size(); ++k)
+                if (v[k].second >= n && (best == v.size() || v[k].second < v[best].second)) best = k;
+            if (best != v.size()) {
+                p = v[best].first;
+                cap = v[best].second;
+                f.kept[dev] -= cap;
+                v.erase(v.begin() + (long)best);
+                return hipSuccess;
+            }
+        }
+        hipError_t e = hipMalloc(&p, n);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            hc_release_cached();
+            e = hipMalloc(&p, n);
+        }
+        cap = e == hipSuccess ? n : 0;
+        if (e != hipSuccess) p = nullptr;
+        return e;
+    }
     template <class T>
     T *as() const
     {
@@ -179,7 +245,10 @@ int decompress_impl(const uint8_t *in, uint64_t n, std::vector<uint8_t> &res)
     }
     // main.cpp:114-125: FGK -> adaptive block revert -> [diff revert]; the matrix size is in
     // the adaptive header, so guess, and rerun with the size the device reports if short
+    // W H <= 64.5 count for adaptive streams too (4 symbols expand to <= 258 bytes)
+    const uint64_t most = count * 65 + 8;
     uint64_t cap = n * 16 > (1u << 20) ? n * 16 : (1u << 20);
+    if (cap > most) cap = most;
     for (int pass = 0; pass < 2; ++pass) {
         DevBuf dout;
         HC_CK(dout.alloc(cap));
@@ -298,6 +367,8 @@ int hc_compress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const ui
         return HC_ERR_ARG;
     if (flags & ~(HC_FLAG_DIFF | HC_FLAG_ADAPT)) return HC_ERR_ARG;
     if (!aligned4(in) || !aligned4(out) || (reinterpret_cast<uintptr_t>(work) & 15u)) return HC_ERR_ARG;
+    // the workspace's fixed part (per-stream metadata, work lists) must fit whatever the sizes
+    if (work_bytes < hc::adapt_encode_work_bound(0, n_streams)) return HC_ERR_ARG;
     Batch b{in, in_offs, in_lens, n_streams, out, out_offs, out_caps, out_lens, status, flags & HC_FLAG_DIFF};
     const hipError_t e = hc::adapt_encode_batch(b, widths, work, work_bytes, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? HC_OK : HC_ERR_DEVICE;
@@ -312,6 +383,7 @@ int hc_decompress_adapt_batch(const uint8_t *in, const uint64_t *in_offs, const 
     if (!in || !in_offs || !in_lens || !out || !out_offs || !out_caps || !out_lens || !status || !work)
         return HC_ERR_ARG;
     if (!aligned4(in) || !aligned4(out) || (reinterpret_cast<uintptr_t>(work) & 15u)) return HC_ERR_ARG;
+    if (work_bytes < hc::adapt_decode_work_bound(0, 0, n_streams)) return HC_ERR_ARG;
     Batch b{in, in_offs, in_lens, n_streams, out, out_offs, out_caps, out_lens, status, 0};
     const hipError_t e = hc::adapt_decode_batch(b, work, work_bytes, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? HC_OK : HC_ERR_DEVICE;
@@ -340,13 +412,33 @@ int hc_device_info(char *buf, uint64_t cap)
 
 int hc_device_ok(void)
 {
+    // the answer per device never changes: asked once per device (hipGetDeviceProperties is not
+    // cheap next to a small single-buffer call)
+    static std::atomic<int> known[64];  // 0 unknown, 1 gfx950, 2 other
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+    if (dev < 64 && known[dev].load(std::memory_order_relaxed)) return known[dev].load(std::memory_order_relaxed) == 1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-    return strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+    const int ok = strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+    if (dev < 64) known[dev].store(ok ? 1 : 2, std::memory_order_relaxed);
+    return ok;
+}
+
+void hc_release_cached(void)
+{
+    FreeList &f = free_list();
+    {
+        std::lock_guard<std::mutex> lk(f.mu);
+        for (int d = 0; d < 64; ++d) {
+            for (auto &b : f.bufs[d]) (void)hipFree(b.first);
+            f.bufs[d].clear();
+            f.kept[d] = 0;
+        }
+    }
+    hc::pipe_release();
 }
 
 }  // extern "C"

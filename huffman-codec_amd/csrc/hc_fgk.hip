@@ -33,25 +33,38 @@ extern "C" __device__ int amdgcn_writelane(int x, int l, int v) __asm("llvm.amdg
 
 namespace hc {
 
-// Diagnostic: when non-null, every FGK wave records (start, end, HW_ID | XCC_ID << 16) at
-// [3 * stream] (scripts/residency.py measures how many waves share each SIMD). Set by
-// hc_debug_set_trace (not part of include/hcodec.h); null in normal use.
+// Test and diagnostic hooks exist only in the debug build (libhcodec_dbg.so, -DHC_DEBUG_HOOKS;
+// tests and bench.py's stage pass load it). The shipping libhcodec.so has no mutable globals:
+// its windows, tree layouts and encoder modes are the constants below.
+#if defined(HC_PROF) && !defined(HC_DEBUG_HOOKS)
+#define HC_DEBUG_HOOKS 1
+#endif
+#ifdef HC_DEBUG_HOOKS
+// when non-null, every FGK wave records (start, end, HW_ID | XCC_ID << 16) at [3 * stream]
+// (scripts/residency.py measures how many waves share each SIMD); hc_debug_set_trace
 __device__ uint64_t *g_trace = nullptr;
-
-// Streams are addressed through buffer descriptors, whose offsets are 32-bit: each stream's input
-// and output are reached through windows that slide forward by whole multiples of 256 bytes
-// once the offset inside them passes g_window (1 GiB; hc_debug_set_window shrinks it so that
-// tests cross many window edges on small streams), so streams of any length fit.
+// the buffer window (below); hc_debug_set_window shrinks it so that tests cross many window
+// edges on small streams
 __device__ uint32_t g_window = 1u << 30;
-
-// Diagnostic: the lowest tree layout (0 narrow, 1 wide, 2 huge) any stream may use; set by
-// hc_debug_set_min_tree so that tests run the wide and huge kernels on small streams. The
-// launchers pass it in Batch::min_tree.
+// the lowest tree layout (0 narrow, 1 wide, 2 huge) any stream may use (hc_debug_set_min_tree:
+// tests run the wide and huge kernels on small streams); the launchers pass it in Batch::min_tree
 static uint32_t g_min_tree = 0;
-
-// Encoder mode for narrow / wide streams: 0 = per stream by enc_mode_kernel (default), 1 = path
+// encoder mode for narrow / wide streams: 0 = per stream by enc_mode_kernel (default), 1 = path
 // cache for all, 2 = tables for all (hc_debug_set_enc_tab; tests run both on every input)
 static uint32_t g_enc_tab = 0;
+__device__ __forceinline__ uint64_t *trace_buf() { return g_trace; }
+__device__ __forceinline__ uint32_t window_bytes() { return __builtin_amdgcn_readfirstlane(g_window); }
+static uint32_t min_tree() { return g_min_tree; }
+static uint32_t enc_tab() { return g_enc_tab; }
+#else
+__device__ __forceinline__ uint64_t *trace_buf() { return nullptr; }
+__device__ __forceinline__ uint32_t window_bytes() { return 1u << 30; }
+static uint32_t min_tree() { return 0; }
+static uint32_t enc_tab() { return 0; }
+#endif
+// Streams are addressed through buffer descriptors, whose offsets are 32-bit: each stream's input
+// and output are reached through windows that slide forward by whole multiples of 256 bytes
+// once the offset inside them passes window_bytes() (1 GiB), so streams of any length fit.
 
 // the tree layout for a stream of at most `max_sym` FGK symbols
 __device__ __forceinline__ uint32_t tree_kind(uint64_t max_sym, uint32_t lo)
@@ -64,7 +77,7 @@ namespace {
 
 __device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t lane)
 {
-    uint64_t *const tr = g_trace;
+    uint64_t *const tr = trace_buf();
 #ifdef HC_PROF
     return;  // the buffer holds the path profile (prof_store)
 #endif
@@ -93,7 +106,7 @@ __device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t l
 __device__ __forceinline__ void prof_store(uint32_t sid, uint64_t t0, uint64_t pacc, uint32_t lane)
 {
 #ifdef HC_PROF
-    uint64_t *const tr = g_trace;
+    uint64_t *const tr = trace_buf();
     if (tr != nullptr && lane < 8) tr[8 * sid + lane] = lane == 0 ? __builtin_amdgcn_s_memtime() - t0 : pacc;
 #endif
 }
@@ -1065,7 +1078,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     if (tree_kind(max_sym, bt.min_tree) != (uint32_t)kW) return;
     // narrow and wide: the cache and the table launches split the streams (enc_mode_kernel)
     if (kW <= 1 && (uni(bt.status[sid]) == kModeTables) != kTab) return;
-    const uint32_t window = uni(g_window);
+    const uint32_t window = window_bytes();
 
     Fgk<kW, false, kTab> fgk(trees[wv], lane);
     RecSink sink;
@@ -1593,7 +1606,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     in.rs = rin;
     in.ibase = 0;
     in.lane = lane;
-    const uint32_t window = uni(g_window);
+    const uint32_t window = window_bytes();
     in.cbase = 0;
     in.chunk = __builtin_bswap32(hdr);
     in.nxt = buf_load(rin, 256 + lane * 4);
@@ -1808,8 +1821,8 @@ static uint32_t table_slots()
 template <int kSrc>
 static void launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipStream_t st)
 {
-    enc_mode_kernel<kSrc><<<(b.n + 3) / 4, 256, 0, st>>>(b, b.n <= table_slots() ? 1u : 0u, g_enc_tab);
-    if (!g_enc_tab) enc_mode_vote_kernel<<<1, 1024, 0, st>>>(b);
+    enc_mode_kernel<kSrc><<<(b.n + 3) / 4, 256, 0, st>>>(b, b.n <= table_slots() ? 1u : 0u, enc_tab());
+    if (!enc_tab()) enc_mode_vote_kernel<<<1, 1024, 0, st>>>(b);
     encode_kernel<0, kSrc><<<grid, block, 0, st>>>(b);
     encode_kernel<0, kSrc, true><<<grid, block, 0, st>>>(b);
     encode_kernel<1, kSrc><<<grid, block, 0, st>>>(b);
@@ -1821,7 +1834,7 @@ hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st)
 {
     if (b0.n == 0) return hipSuccess;
     Batch b = b0;
-    b.min_tree = g_min_tree;
+    b.min_tree = min_tree();
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
     // enc_mode_kernel marks each stream for the cache or the table launch; then one launch per
     // tree layout and mode, each stream coded by exactly one of them (tree_kind, the mark)
@@ -1837,7 +1850,7 @@ hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)
 {
     if (b0.n == 0) return hipSuccess;
     Batch b = b0;
-    b.min_tree = g_min_tree;
+    b.min_tree = min_tree();
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
     if (dst == DST_RAW) {
         decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
@@ -1853,6 +1866,7 @@ hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)
 
 }  // namespace hc
 
+#ifdef HC_DEBUG_HOOKS
 extern "C" int hc_debug_set_window(uint32_t bytes)
 {
     // a multiple of 256 in [4096, 2^30]: the descriptor windows of every later FGK launch
@@ -1880,3 +1894,4 @@ extern "C" int hc_debug_set_trace(void *dev_buf)
     uint64_t *p = static_cast<uint64_t *>(dev_buf);
     return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_trace), &p, sizeof(p)) == hipSuccess ? 0 : HC_ERR_DEVICE;
 }
+#endif  // HC_DEBUG_HOOKS

@@ -48,4 +48,8 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
 uint64_t adapt_encode_work_bound(uint64_t total_in, uint32_t n);
 uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t n);
 
+// frees the host-batch pipeline slots' cached buffers (hc_release_cached; slots in use by a
+// running call are left alone)
+void pipe_release();
+
 }  // namespace hc

@@ -85,7 +85,13 @@ template <class T>
 struct Dev {
     T *p = nullptr;
     uint64_t cap = 0;
-    ~Dev() { if (p) (void)hipFree(p); }
+    ~Dev() { drop(); }
+    void drop()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
     hipError_t need(uint64_t n)
     {
         if (n <= cap) return hipSuccess;
@@ -102,7 +108,13 @@ template <class T>
 struct Pinned {
     T *p = nullptr;
     uint64_t cap = 0;
-    ~Pinned() { if (p) (void)hipHostFree(p); }
+    ~Pinned() { drop(); }
+    void drop()
+    {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
     hipError_t need(uint64_t n)
     {
         if (n <= cap) return hipSuccess;
@@ -132,12 +144,49 @@ struct Slot {
         if (meta_done) (void)hipEventDestroy(meta_done);
         if (st) (void)hipStreamDestroy(st);
     }
+    uint64_t device_bytes() const
+    {
+        return din.cap + dout.cap + dpacked.cap + dtmp.cap + dwork.cap + 8 * (dup.cap + dlens.cap + dkept.cap + dat.cap) +
+               4 * dstatus.cap;
+    }
+    // free the buffers (the stream and event stay); the slot must be idle
+    void release()
+    {
+        hin.drop();
+        hpacked.drop();
+        hup.drop();
+        hdown.drop();
+        din.drop();
+        dout.drop();
+        dpacked.drop();
+        dtmp.drop();
+        dwork.drop();
+        dup.drop();
+        dlens.drop();
+        dkept.drop();
+        dat.drop();
+        dstatus.drop();
+    }
 };
 
+// The two slots of one device, kept between calls (allocating and pinning a GiB per call cost
+// more than the coding). One pool per device: a slot's stream and buffers belong to the device
+// that was current when they were made.
 struct Pool {
     std::mutex mu;
     Slot slots[2];
 };
+constexpr int kMaxDevices = 64;
+std::mutex g_pools_mu;
+Pool *g_pools[kMaxDevices];  // made on first use, never destroyed (the HIP runtime may be gone at exit)
+
+Pool *pool_of(int dev)
+{
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pools_mu);
+    if (!g_pools[dev]) g_pools[dev] = new Pool;
+    return g_pools[dev];
+}
 
 struct Job {
     bool encode;
@@ -284,6 +333,8 @@ uint64_t env_u64(const char *name, uint64_t dflt)
     return x ? x : dflt;
 }
 
+int run_slots(Job &j, uint32_t n, Slot *slots);
+
 int run(Job &j, uint32_t n)
 {
     if (n == 0) return HC_OK;
@@ -291,17 +342,36 @@ int run(Job &j, uint32_t n)
     for (uint32_t i = 0; i < n; ++i)
         if ((!j.in[i] && j.in_lens[i]) || (!j.out[i] && j.out_caps[i])) return HC_ERR_ARG;
     if (!hc_device_ok()) return HC_ERR_DEVICE;
+    j.dcap.resize(n);
+    for (uint32_t i = 0; i < n; ++i) j.dcap[i] = guess_cap(j, i);
+    // the current device's two slots (kept between calls); a concurrent call on the same device
+    // gets slots of its own, freed when it returns
+    int dev = -1;
+    PIPE_CK(hipGetDevice(&dev));
+    Pool *const pool = pool_of(dev);
+    std::unique_lock<std::mutex> lk;
+    if (pool) lk = std::unique_lock<std::mutex>(pool->mu, std::try_to_lock);
+    Slot local[2];
+    Slot *const slots = lk.owns_lock() ? pool->slots : local;
+    const int rc = run_slots(j, n, slots);
+    // the kept slots give back what is above HC_PIPE_KEEP_BYTES (default 8 GiB of device
+    // buffers; e.g. after a large adaptive decode) -- their work is done once run_slots returns
+    if (lk.owns_lock()) {
+        const uint64_t keep = env_u64("HC_PIPE_KEEP_BYTES", 8ull << 30);
+        if (slots[0].device_bytes() + slots[1].device_bytes() > keep)
+            for (int k = 0; k < 2; ++k) {
+                (void)hipStreamSynchronize(slots[k].st);
+                slots[k].release();
+            }
+    }
+    return rc;
+}
+
+int run_slots(Job &j, uint32_t n, Slot *slots)
+{
     // sub-batch limits: input bytes and streams per slot (HC_PIPE_BYTES / HC_PIPE_STREAMS)
     const uint64_t max_bytes = env_u64("HC_PIPE_BYTES", 1ull << 30);
     const uint64_t max_streams = env_u64("HC_PIPE_STREAMS", 8192);
-    j.dcap.resize(n);
-    for (uint32_t i = 0; i < n; ++i) j.dcap[i] = guess_cap(j, i);
-    // the two slots and their pinned / device buffers persist between calls (allocating and
-    // pinning a GiB per call cost more than the coding); a concurrent call gets its own
-    static Pool *const pool = new Pool;  // never freed: the HIP runtime may be gone at exit
-    std::unique_lock<std::mutex> lk(pool->mu, std::try_to_lock);
-    Slot local[2];
-    Slot *const slots = lk.owns_lock() ? pool->slots : local;
     for (int k = 0; k < 2; ++k) {
         Slot &s = slots[k];
         s.busy = false;
@@ -355,6 +425,22 @@ int run(Job &j, uint32_t n)
 }
 
 }  // namespace
+
+namespace hc {
+void pipe_release()
+{
+    std::lock_guard<std::mutex> lk(g_pools_mu);
+    for (Pool *p : g_pools) {
+        if (!p) continue;
+        std::unique_lock<std::mutex> pl(p->mu, std::try_to_lock);
+        if (!pl.owns_lock()) continue;  // a call is using it
+        for (Slot &s : p->slots) {
+            if (s.st) (void)hipStreamSynchronize(s.st);
+            s.release();
+        }
+    }
+}
+}  // namespace hc
 
 extern "C" {
 

@@ -12,6 +12,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 # HC_LIB_PATH: another build of the same library (A/B timing of kernel variants in one run)
 LIB_PATH = os.environ.get("HC_LIB_PATH") or os.path.join(PKG, "lib", "libhcodec.so")
+# the same sources built with the test / diagnostic hooks (-DHC_DEBUG_HOOKS): the hc_debug_*
+# entry points exist only there, so the shipping library carries no mutable global state
+DBG_LIB_PATH = os.environ.get("HC_DBG_LIB_PATH") or os.path.join(PKG, "lib", "libhcodec_dbg.so")
 CLI_PATH = os.path.join(PKG, "bin", "huffman-codec")
 BATCH_CLI_PATH = os.path.join(PKG, "bin", "huffman-codec-batch")
 INCLUDE_DIR = os.path.join(os.path.dirname(PKG), "include")
@@ -39,7 +42,8 @@ HC_FLAG_ADAPT = 0x40
 
 SYNTH = {"noise": 0, "grad": 1, "photo": 2}
 
-_lib = None
+_libs = {}           # path -> loaded library
+_active = LIB_PATH   # the library every call below goes to (use_debug_build switches it)
 
 
 class HCodecError(RuntimeError):
@@ -51,13 +55,26 @@ def build():
     subprocess.run(["make", "-s", "-C", PKG], check=True)
 
 
+def use_debug_build(on=True):
+    """Route every later call of this module to libhcodec_dbg.so (on) or back to the shipping
+    libhcodec.so (off). Tests that set a debug hook run their calls on the debug build; the two
+    libraries are separate code objects, each with its own device state."""
+    global _active
+    _active = DBG_LIB_PATH if on else LIB_PATH
+    return lib()
+
+
 def lib():
-    """Load libhcodec.so; raise if it has not been built (no fallback path exists)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise HCodecError(f"{LIB_PATH} missing: build it with `make -C {PKG}`")
+    """The active library (libhcodec.so unless use_debug_build); raise if it has not been built
+    (no fallback path exists)."""
+    return _load(_active)
+
+
+def _load(path):
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise HCodecError(f"{path} missing: build it with `make -C {PKG}`")
     # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's). Whichever loads first
     # serves the whole process; loading ours first leaves torch without a GPU. So let torch's
     # runtime load first and libhcodec.so binds to it: one HIP runtime, shared device pointers.
@@ -65,7 +82,7 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     u8p = ctypes.c_void_p
     u64 = ctypes.c_uint64
     vp = ctypes.c_void_p
@@ -95,8 +112,21 @@ def lib():
     L.hc_device_info.argtypes = [ctypes.c_char_p, u64]
     L.hc_device_info.restype = ctypes.c_int
     L.hc_synth_batch.argtypes = [ctypes.c_int, u64, ctypes.c_uint32, u64, u64, vp, u64, vp]
-    _lib = L
+    _libs[path] = L
     return L
+
+
+def _dbg():
+    """the debug build, which must be the active one (a hook set there would otherwise not
+    affect the calls that follow)"""
+    if _active != DBG_LIB_PATH:
+        raise HCodecError("debug hooks need use_debug_build(True) first")
+    return lib()
+
+
+def release_cached():
+    """hc_release_cached: free the library's cached device / pinned buffers"""
+    lib().hc_release_cached()
 
 
 def _buf(data):
@@ -192,14 +222,27 @@ def _work(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+def _check_work(work, device, need):
+    import torch
+    if not (isinstance(work, torch.Tensor) and work.is_cuda and work.device == device
+            and work.dtype == torch.uint8 and work.is_contiguous()):
+        raise ValueError(f"work: expected a contiguous uint8 CUDA tensor on {device}")
+    if work.data_ptr() % 16:
+        raise ValueError("work: must be 16-byte aligned")
+    if work.numel() < need:
+        raise ValueError(f"work: {work.numel()} bytes, the call needs {need}")
+
+
 def compress_adapt_batch(inp, in_offs, in_lens, widths, out, out_offs, out_caps, out_lens, status,
                          use_diff=False, stream=None, work=None):
     """hc_compress_adapt_batch (-a, optionally -m) on CUDA tensors; widths: int64 per matrix.
     The workspace is allocated here unless given (uint8 CUDA tensor)."""
     n = _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status)
     _check_batch(inp, in_offs, widths, out, out_offs, out_caps, out_lens, status)
+    need = int(lib().hc_adapt_compress_work_bound(int(in_lens.sum()), n))
     if work is None:
-        work = _work(lib().hc_adapt_compress_work_bound(int(in_lens.sum()), n), inp.device)
+        work = _work(need, inp.device)
+    _check_work(work, inp.device, need)
     rc = lib().hc_compress_adapt_batch(_dp(inp), _dp(in_offs), _dp(in_lens), _dp(widths), n,
                                        HC_FLAG_DIFF if use_diff else 0, _dp(out), _dp(out_offs), _dp(out_caps),
                                        _dp(out_lens), _dp(status), _dp(work), work.numel(),
@@ -213,8 +256,10 @@ def decompress_adapt_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_l
                            work=None):
     """hc_decompress_adapt_batch on CUDA tensors (adaptive streams -> matrices)."""
     n = _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status)
+    need = int(lib().hc_adapt_decompress_work_bound(int(in_lens.sum()), int(out_caps.sum()), n))
     if work is None:
-        work = _work(lib().hc_adapt_decompress_work_bound(int(in_lens.sum()), int(out_caps.sum()), n), inp.device)
+        work = _work(need, inp.device)
+    _check_work(work, inp.device, need)
     rc = lib().hc_decompress_adapt_batch(_dp(inp), _dp(in_offs), _dp(in_lens), n, _dp(out), _dp(out_offs),
                                          _dp(out_caps), _dp(out_lens), _dp(status), _dp(work), work.numel(),
                                          _stream_handle(stream))
@@ -294,10 +339,10 @@ def synth_batch(kind, k0, n_streams, width, height, out, stride, stream=None):
 
 
 def debug_set_window(nbytes):
-    """Test hook (not part of include/hcodec.h): the FGK kernels reach each stream through buffer
+    """Test hook (debug build only, use_debug_build): the FGK kernels reach each stream through buffer
     windows that slide every `nbytes` (default 1 GiB); a small window makes ordinary streams
     cross many window edges. Affects every later launch in this process."""
-    f = lib().hc_debug_set_window
+    f = _dbg().hc_debug_set_window
     f.argtypes = [ctypes.c_uint32]
     rc = f(int(nbytes))
     if rc:
@@ -305,10 +350,10 @@ def debug_set_window(nbytes):
 
 
 def debug_set_min_tree(kind):
-    """Test hook (not part of include/hcodec.h): the smallest FGK tree layout every later launch
+    """Test hook (debug build only, use_debug_build): the smallest FGK tree layout every later launch
     in this process may use (0 narrow, 1 wide, 2 huge: 64-bit weights), so that small streams
     exercise the kernels otherwise reserved for streams of > 2^22 - 2 / >= 2^32 - 1 symbols."""
-    f = lib().hc_debug_set_min_tree
+    f = _dbg().hc_debug_set_min_tree
     f.argtypes = [ctypes.c_uint32]
     rc = f(int(kind))
     if rc:
@@ -316,10 +361,10 @@ def debug_set_min_tree(kind):
 
 
 def debug_set_enc_tab(mode):
-    """Test hook (not part of include/hcodec.h): how the encoder finds a symbol's code for
+    """Test hook (debug build only, use_debug_build): how the encoder finds a symbol's code for
     narrow / wide streams: 0 per stream from a sample of its alphabet (the default), 1 the path
     cache for every stream, 2 the level tables for every stream."""
-    f = lib().hc_debug_set_enc_tab
+    f = _dbg().hc_debug_set_enc_tab
     f.argtypes = [ctypes.c_uint32]
     rc = f(int(mode))
     if rc:
@@ -327,16 +372,16 @@ def debug_set_enc_tab(mode):
 
 
 def debug_stage_clock(on):
-    """Diagnostic (not part of include/hcodec.h): when on, the batched adaptive calls record a
-    HIP event after each stage; debug_stage_times() reads the last call's stages."""
-    f = lib().hc_debug_stage_clock
+    """Diagnostic (debug build only, use_debug_build): when on, the batched adaptive calls of
+    this thread record a HIP event after each stage; debug_stage_times() reads the last call's."""
+    f = _dbg().hc_debug_stage_clock
     f.argtypes = [ctypes.c_int]
     f(1 if on else 0)
 
 
 def debug_stage_times():
     """[(stage, ms), ...] of the last batched adaptive call (waits for it); needs the clock on"""
-    f = lib().hc_debug_stage_times
+    f = _dbg().hc_debug_stage_times
     f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     names = ctypes.create_string_buffer(1024)
     ms = (ctypes.c_float * 32)()

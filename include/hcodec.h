@@ -163,6 +163,14 @@ int hc_decompress_host_batch(const uint8_t *const *in, const uint64_t *in_lens, 
 int hc_pack_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *lens, uint32_t n_streams,
                   uint8_t *out, const uint64_t *out_offs, void *stream);
 
+/* Allocation caches. The single-buffer API keeps device scratch between calls (per device,
+ * at most 1 GiB each) and the host-buffer batch API keeps its pipeline buffers (per device;
+ * above HC_PIPE_KEEP_BYTES, default 8 GiB, of device buffers they are freed at the end of the
+ * call). These cache memory only: no result depends on them and concurrent calls never share a
+ * buffer. hc_release_cached() frees every cached buffer not in use by a running call (e.g.
+ * before handing the memory to another allocator). */
+void hc_release_cached(void);
+
 /* Library version string and a device check (1 = a gfx950 device is usable). */
 const char *hc_version(void);
 int hc_device_ok(void);

@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "huffman-codec_amd", "python"))
 def main():
     import torch
     import hcodec as hc
+    hc.use_debug_build(True)  # hc_debug_set_enc_tab: debug build only
     dev = torch.device("cuda", 0)
     N = 512 * 512
     cases = [("photo -c", "photo", 4096, False), ("photo -c 8192", "photo", 8192, False),
@@ -56,6 +57,7 @@ def adaptive():
     """the adaptive configs (symbol streams, bit 2): A512 and C4 / C4m"""
     import torch
     import hcodec as hc
+    hc.use_debug_build(True)  # hc_debug_set_enc_tab: debug build only
     dev = torch.device("cuda", 0)
     for name, S, side, diff in (("A512 -a -m", 8192, 512, True), ("A512 -a", 8192, 512, False),
                                 ("C4 -a", 1, 4096, False), ("C4m -a -m", 1, 4096, True)):

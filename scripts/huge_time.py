@@ -1,6 +1,7 @@
 import sys, time, os
 sys.path.insert(0, "huffman-codec_amd/python"); sys.path.insert(0, "oracle")
 import torch, hcodec as hc, oracle, numpy as np
+hc.use_debug_build(True)  # hc_debug_set_min_tree: debug build only
 n = 1 << 26
 pat = torch.tensor([1, 1, 2, 1, 1, 3, 1, 1, 2], dtype=torch.uint8, device="cuda")
 raw = pat.repeat(n // pat.numel() + 1)[:n].contiguous()

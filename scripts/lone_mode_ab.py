@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "huffman-codec_amd", "python"))
 def main():
     import torch
     import hcodec as hc
+    hc.use_debug_build(True)  # hc_debug_set_enc_tab: debug build only
     dev = torch.device("cuda", 0)
     i64 = dict(dtype=torch.int64, device=dev)
     for name, side, adapt, diff in (("C2", 512, False, True), ("C3-1", 512, False, False), ("C4m", 4096, True, True),

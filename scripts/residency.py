@@ -92,7 +92,7 @@ def main():
     args = ap.parse_args()
     import torch
     import hcodec as hc
-    L = hc.lib()
+    L = hc.use_debug_build(True)  # hc_debug_set_trace: debug build only
     L.hc_debug_set_trace.argtypes = [ctypes.c_void_p]
     S, N = args.streams, 512 * 512
     dev = torch.device("cuda", 0)

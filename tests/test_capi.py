@@ -55,3 +55,38 @@ def test_headers_compile_as_c(hc, tmp_path):
     src.write_text('#include "hcodec.h"\n#include "hcodec_synth.h"\nint main(void){return HC_OK;}\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", hc.INCLUDE_DIR, str(src), "-o",
                     str(tmp_path / "t")], check=True)
+
+
+def test_shipping_library_has_no_hooks(hc):
+    """The test / diagnostic hooks (hc_debug_*: forced tree layouts and encoder modes, shrunk
+    buffer windows, traces, the adaptive stage clock) live in libhcodec_dbg.so only: the shipping
+    libhcodec.so exports none of them and carries none of their global variables, so its entry
+    points keep hcodec.h's "no hidden global state" (the reference: one HuffTree per call,
+    transform.cpp:366,388)."""
+    def syms(path, flags):
+        out = subprocess.run(["nm", "-C", *flags, path], capture_output=True, text=True, check=True).stdout
+        return out
+    ship = syms(hc.LIB_PATH, ["-D", "--defined-only"])
+    assert "hc_debug" not in ship
+    allsyms = syms(hc.LIB_PATH, [])
+    for g in ("g_window", "g_min_tree", "g_enc_tab", "g_trace", "g_clock"):
+        assert g not in allsyms, g
+    dbg = syms(hc.DBG_LIB_PATH, ["-D", "--defined-only"])
+    for f in ("hc_debug_set_window", "hc_debug_set_min_tree", "hc_debug_set_enc_tab", "hc_debug_stage_clock",
+              "hc_debug_stage_times", "hc_debug_set_trace"):
+        assert f in dbg, f
+    with pytest.raises(hc.HCodecError):  # hooks refuse to run against the shipping build
+        hc.debug_set_min_tree(1)
+
+
+def test_adapt_batch_rejects_short_workspace(hc):
+    """hc_*_adapt_batch check work_bytes against the workspace's fixed part before any device
+    work (a short workspace would otherwise be written out of bounds)"""
+    L = hc.lib()
+    one = ctypes.c_void_p(256)
+    need = int(L.hc_adapt_compress_work_bound(0, 4))
+    assert L.hc_compress_adapt_batch(one, one, one, one, 4, 0, one, one, one, one, one, one, need - 1,
+                                     ctypes.c_void_p(0)) == hc.HC_ERR_ARG
+    need = int(L.hc_adapt_decompress_work_bound(0, 0, 4))
+    assert L.hc_decompress_adapt_batch(one, one, one, 4, one, one, one, one, one, one, need - 1,
+                                       ctypes.c_void_p(0)) == hc.HC_ERR_ARG

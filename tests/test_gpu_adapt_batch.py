@@ -147,6 +147,7 @@ def test_stage_clock(gpu, hc, oracle_mod):
     in launch order, with non-negative times; off again afterwards (the calls unchanged)"""
     torch = gpu
     raws = [oracle_mod.synth("photo", k, 256, 256).tobytes() for k in range(4)]
+    hc.use_debug_build(True)  # the clock exists in the debug build only
     hc.debug_stage_clock(True)
     try:
         st, enc, _ = compress_adapt_batch(hc, torch, raws, [256] * 4, True)
@@ -161,5 +162,10 @@ def test_stage_clock(gpu, hc, oracle_mod):
     assert [n for n, _ in dec_stages] == ["dec_plan", "fgk_decode", "dec_header", "bounds", "unblock_tile",
                                          "unblock", "chunk_sum", "chunk_scan", "undiff", "dec_final"]
     assert all(ms >= 0 for _, ms in enc_stages + dec_stages)
-    with pytest.raises(hc.HCodecError):
-        hc.debug_stage_times()
+    try:
+        with pytest.raises(hc.HCodecError):
+            hc.debug_stage_times()
+    finally:
+        hc.use_debug_build(False)
+    with pytest.raises(hc.HCodecError):  # the shipping build has no hooks
+        hc.debug_stage_clock(True)

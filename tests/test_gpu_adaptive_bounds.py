@@ -110,3 +110,29 @@ def test_bounds_other_block_sizes_vs_oracle(gpu, hc, oracle_mod):
             assert got == want, (case, w, h, b)
         seen.add(st)
     assert 0 in seen and len(seen) >= 2, seen
+
+
+def test_bounds_narrow_forged_matrices_vs_oracle(gpu, hc, oracle_mod):
+    """forged headers the encoder never writes: matrices 1..3 wide (or high) with B = 8 / 16,
+    whose tile block rows outnumber the group-start entries a W, H >= 8 stream needs (the decoder
+    then takes K-block groups instead). Decoded through the batched API with the exact output
+    capacity (W * H) and through the single-buffer API; status and bytes as the oracle's
+    (headers.cpp:65-105 accepts any W, H; transform.cpp:330-361)."""
+    from gpu_batch import decompress_adapt_batch
+    torch = gpu
+    rng = np.random.default_rng(31)
+    streams, sizes, wants = [], [], []
+    for (w, h, b) in [(1, 3000, 8), (2, 2000, 8), (3, 1200, 8), (1, 4000, 16), (2, 900, 16), (3000, 1, 8),
+                      (3, 3, 8), (1, 1, 8)]:
+        hdr, body = adaptive_stream(rng, w, h, b)
+        data = container(oracle_mod, hdr + body)
+        want_st, want = oracle_mod.decompress(data)
+        assert want_st == 0, (w, h, b)
+        st, got = hc.decompress(data)
+        assert st == 0 and got == want, (w, h, b)
+        streams.append(data)
+        sizes.append(w * h)
+        wants.append(want)
+    dst, dec, _ = decompress_adapt_batch(hc, torch, streams, sizes)
+    assert dst == [0] * len(streams)
+    assert dec == wants

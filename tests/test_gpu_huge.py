@@ -31,9 +31,11 @@ def sha(b):
 
 @pytest.fixture(params=[1, 2], ids=["wide", "huge"])
 def tree(request, gpu, hc):
+    hc.use_debug_build(True)  # the hook exists in the debug build only
     hc.debug_set_min_tree(request.param)
     yield request.param
     hc.debug_set_min_tree(0)
+    hc.use_debug_build(False)
 
 
 def test_forced_tree_digests(gpu, hc, oracle_mod, digests, tree):

@@ -23,9 +23,11 @@ def sha(b):
 
 @pytest.fixture(params=[2, 1, 0], ids=["tables", "cache", "auto"])
 def enc_mode(request, gpu, hc):
+    hc.use_debug_build(True)  # the hook exists in the debug build only
     hc.debug_set_enc_tab(request.param)
     yield request.param
     hc.debug_set_enc_tab(0)
+    hc.use_debug_build(False)
 
 
 def test_enc_mode_digests(gpu, hc, oracle_mod, digests, enc_mode):

@@ -26,9 +26,11 @@ def sha(b):
 
 @pytest.fixture
 def small_window(gpu, hc):
+    hc.use_debug_build(True)  # the hook exists in the debug build only
     hc.debug_set_window(4096)
     yield
     hc.debug_set_window(1 << 30)
+    hc.use_debug_build(False)
 
 
 def test_small_window_batch_vs_oracle(gpu, hc, oracle_mod, small_window):
