@@ -72,6 +72,44 @@ def src_sha():
         return sha(f.read())[:16]
 
 
+def host_cpus():
+    """The host's CPUs: the model, the hardware threads and physical cores of the node, and how
+    many this process may use (affinity and the cgroup CPU quota: a GPU box gives one GPU's job a
+    share of the node's cores)"""
+    info = {"cpu_model": "?", "node_threads": os.cpu_count() or 1}
+    cores = set()
+    try:
+        phys = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and info["cpu_model"] == "?":
+                    info["cpu_model"] = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    cores.add((phys, v))
+    except OSError:
+        pass
+    info["physical_cores"] = len(cores) or info["node_threads"]
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = info["node_threads"]
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    info["affinity_threads"] = aff
+    info["cgroup_cpu_quota"] = quota
+    info["usable"] = max(1, min(aff, int(quota) if quota else aff))
+    return info
+
+
 def cpu_baseline(args, cores, gpu_encoded):
     """The reference binary itself (oracle/_ref: the Makefile build, -O0, and the same sources
     at -O2) on a bounded sample of the same workload, one process per stream over `cores` host
@@ -126,7 +164,7 @@ def cpu_baseline(args, cores, gpu_encoded):
     return {"value": main_leg["value"], "unit": "GiB/s", "cores": cores, "kind": "reference",
             "build": main_leg["build"],
             "sample": f"{sample} x 512x512 {args.kind} streams (k = 0..{sample - 1}), {' '.join(mode)} then -d, "
-                      f"one process per stream on {cores} host cores (oracle/_ref, compiled from the reference "
+                      f"one process per stream on the {cores} host CPUs this job may use (oracle/_ref, compiled from the reference "
                       f"sources; value = the {main_leg['build']} build, every build in legs)",
             "legs": legs,
             "bit_exact_vs_gpu": all(l["gpu_bytes_identical"] and l["round_trip"] for l in legs)}
@@ -135,13 +173,19 @@ def cpu_baseline(args, cores, gpu_encoded):
 class Batch:
     """S synthetic 512x512 streams resident in HBM with encode / decode buffers."""
 
-    def __init__(self, torch, hc, dev, kind, k0, S, use_diff, side=512):
+    def __init__(self, torch, hc, dev, kind, k0, S, use_diff, side=512, kinds=None):
         self.torch, self.hc, self.dev, self.S, self.use_diff = torch, hc, dev, S, use_diff
         self.N = side * side
         N = self.N
         self.cap = 2 * N + 4096
         self.raw = torch.empty(S * N, dtype=torch.uint8, device=dev)
-        hc.synth_batch(kind, k0, S, side, side, self.raw, N)
+        if kinds is None:
+            hc.synth_batch(kind, k0, S, side, side, self.raw, N)
+        else:  # [(kind, count), ...] one after another (a mixed batch)
+            at = 0
+            for kd, cnt in kinds:
+                hc.synth_batch(kd, k0, cnt, side, side, self.raw[at * N:(at + cnt) * N], N)
+                at += cnt
         i64 = dict(dtype=torch.int64, device=dev)
         self.offs = torch.arange(S, **i64) * N
         self.lens = torch.full((S,), N, **i64)
@@ -342,6 +386,13 @@ def adapt_stages(torch, hc, b, stream):
                 gbs = nb / (ms * 1e-3) / 1e9
                 e.update({"alg_bytes": nb, "GBps": round(gbs, 1), "hbm_frac": round(gbs / 8000.0, 4)})
             d[name] = e
+        if direction == "decode":  # the serial and the parallel boundary passes together
+            ms = sum(v["ms"] for k, v in d.items() if k == "bounds" or k.startswith("par_"))
+            if ms > 0:
+                gbs = syms / (ms * 1e-3) / 1e9
+                d["block_boundaries"] = {"ms": round(ms, 4), "alg_bytes": syms, "GBps": round(gbs, 1),
+                                         "hbm_frac": round(gbs / 8000.0, 4),
+                                         "stages": "bounds + par_fsm/entry/z/scan/walk/fix"}
         out[direction] = d
     return out
 
@@ -372,6 +423,26 @@ def config_adapt(torch, hc, dev, stream, what, S, side, use_diff, steps, digests
     return out, bad
 
 
+def config_mixed(torch, hc, dev, stream, photos=6144, noises=2048):
+    """a batch mixing two alphabets (photo -c -m: the encoder's path cache; noise -c -m: its level
+    tables), encoded as one batch and as its two parts: each stream's mode is its own and the
+    two modes' launches run side by side, so the mixed batch should cost no more than the parts"""
+    out, bad = {"what": f"{photos} photo + {noises} noise 512x512 -c -m in one batch vs the two parts", "mode": "-c -m"}, 0
+    for name, kinds, S in (("mixed", [("photo", photos), ("noise", noises)], photos + noises),
+                           ("photo_part", None, photos), ("noise_part", None, noises)):
+        kind = "noise" if name == "noise_part" else "photo"
+        b = Batch(torch, hc, dev, kind, 0, S, True, kinds=kinds)
+        _, enc_ms, dec_ms = timed(torch, b, stream, 2, 1)
+        bad += b.bad()
+        out[name] = {"streams": S, "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4)}
+        del b
+        torch.cuda.empty_cache()
+    out["encode_mixed_over_parts"] = round(out["mixed"]["encode_ms"] /
+                                           (out["photo_part"]["encode_ms"] + out["noise_part"]["encode_ms"]), 4)
+    out["round_trip_exact"] = bad == 0
+    return out, bad
+
+
 def run_configs(torch, hc, dev, stream, only):
     with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
         digests = json.load(f)
@@ -386,6 +457,9 @@ def run_configs(torch, hc, dev, stream, only):
         if only and name not in only:
             continue
         res[name], b = config_batch(torch, hc, dev, stream, name, what, kind, S, d, steps, digests)
+        bad += b
+    if not only or "mixed" in only:
+        res["mixed"], b = config_mixed(torch, hc, dev, stream)
         bad += b
     aplan = [
         ("C4", "1 x 4096x4096 photo -c -a -w 4096 (one matrix: one FGK wavefront), device-resident", 1, 4096, False, 2),
@@ -511,9 +585,17 @@ def main():
     if args.gather:
         result["gather"] = time_gather(torch, hcdist, b, dev, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cores = min(16, os.cpu_count() or 1)
+        host = host_cpus()
+        cores = host["usable"]
         sample = min(args.cpu_sample or 8 * cores, S)
         cb = cpu_baseline(args, cores, [b.encoded(k) for k in range(sample)])
+        if cb is not None:
+            cb.update(host)
+            # the node's physical cores at the measured per-process rate (one stream per process
+            # scales linearly until the cores run out; SMT threads beyond them add little)
+            cb["node_estimate"] = {"value": cb["value"] / cores * host["physical_cores"], "unit": "GiB/s",
+                                   "cores": host["physical_cores"],
+                                   "how": "measured value / cores used x the node's physical cores"}
         if cb is not None:
             if not cb["bit_exact_vs_gpu"]:
                 raise SystemExit("GPU encodings differ from the reference binary's on the sampled streams")

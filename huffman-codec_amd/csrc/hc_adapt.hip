@@ -87,6 +87,14 @@ struct AMeta {
     uint32_t pad2;
     uint64_t tiles;                  // decode: tiles (mode 0)
     uint64_t ents;                   // decode: group-start entries reserved at `starts`
+    // decode, parallel block-boundary pass (bounds_par: streams of >= kParMin block symbols)
+    uint32_t pcap;                   // the slab holds the pass's data (dec_plan)
+    uint32_t par;                    // the stream takes the pass (dec_header)
+    uint32_t pfall;                  // par_scan gave up (a window past kWinCap): par_fix re-runs all
+    uint32_t pad3;
+    uint64_t psub, pchk, pz, pzi, ps0;  // workspace offsets: sub-chunk records, chunk records, Z, Z info, s0
+    uint64_t nsub, nchk, preruns;
+    uint64_t pdiag[8];               // debug build: par_scan cycle counts (scripts/par_diag.py)
 };
 
 // workspace: [meta n][idx0 n+1][idx1 n+1][idx2 n+1][idx3 n+1][sym_offs n][sym_lens n][sym_caps n]
@@ -1544,6 +1552,48 @@ struct DecArgs {
     int32_t *status;
 };
 
+constexpr uint32_t kSub = 2048;        // symbols per sub-chunk
+constexpr uint32_t kSubPerChunk = 8;   // sub-chunks per walked chunk (16384 symbols)
+constexpr uint32_t kZcap = 512;        // Z entries a sub-chunk keeps (more: every symbol is tested)
+constexpr uint32_t kWinLook = 64;      // par_z: a reset machine must rejoin s0 within this
+constexpr uint32_t kWinCap = 4096;     // par_scan: a longer window falls back to the serial pass
+constexpr uint64_t kParMin = 1ull << 20;  // block symbols from which a stream takes this pass
+#ifdef HC_DEBUG_HOOKS
+// debug build: hc_debug_set_par_min lowers the threshold so that tests run the pass on small
+// streams (all of the serial pass's edge cases through the parallel one)
+__device__ uint64_t g_par_min = kParMin;
+__device__ __forceinline__ uint64_t par_min() { return g_par_min; }
+#else
+__device__ __forceinline__ uint64_t par_min() { return kParMin; }
+#endif
+constexpr uint32_t kDense = 0xFFFFFFFFu;
+
+struct PSub {
+    uint32_t F;   // composed transition function of the sub-chunk's symbols
+    uint32_t s0;  // no-reset state before its first symbol
+    uint32_t L;   // no-reset output bytes of its symbols
+    uint32_t zn;  // Z entries (kDense: too many, all symbols are tested)
+    uint64_t o0;  // no-reset output offset at its first symbol (par_scan)
+};
+struct PChk {
+    uint64_t q0, o_in;  // par_scan: the walk starts at symbol q0 <= the chunk start, offset o_in,
+    uint32_t r_in;      // state r_in
+    uint32_t st;        // par_walk: status
+    uint64_t o_q;       // the process at the chunk start (offset, state; r_q 0xFF: not reached)
+    uint32_t r_q, r_out;
+    uint64_t o_out;     // ... and at its end
+};
+
+// parallel block-boundary pass (bounds_par below): the data a stream of `cap` symbols reserves
+// for it in its slab (none below kParMin symbols)
+__device__ inline uint64_t par_subs(uint64_t cap) { return cap >= par_min() ? cdiv(cap, kSub) : 0; }
+__device__ inline uint64_t par_bytes(uint64_t cap)
+{
+    const uint64_t ns = par_subs(cap);
+    return align_up(sizeof(PSub) * ns, 16) + align_up(sizeof(PChk) * cdiv(ns, kSubPerChunk), 16) +
+           2 * align_up(4ull * kZcap * ns, 16) + align_up(kSub / 4 * ns, 16);
+}
+
 // u64 block-start entries per stream (W H <= cap, W, H >= 8): mode 0 ceil(H/B) ceil(W/128) <=
 // (H/8 + 1)(W/128 + 1) <= WH/1024 + WH/64 + WH/1024 + 1; mode 1 far fewer; mode 2
 // <= 4 W H / 1024 + 1 (dec_header_kernel)
@@ -1568,7 +1618,8 @@ __global__ __launch_bounds__(1024) void dec_plan_kernel(DecArgs a, Ws ws)
             for (int b = 7; b >= 0; --b) count = count << 8 | p[b];
         const bool ok = len >= 9 && (p[8] & HC_FLAG_ADAPT);
         const uint64_t oc = a.out_caps[i];
-        v[0] = ok ? align_up(sym_cap(count, len) + 64, 16) + align_up(8 * group_entries_bound(oc) + oc / kChunk + 16, 16)
+        const uint64_t cap = sym_cap(count, len);
+        v[0] = ok ? align_up(cap + 64, 16) + align_up(8 * group_entries_bound(oc) + oc / kChunk + 16, 16) + par_bytes(cap)
                   : 0;
     };
     auto put = [&](uint32_t i, const uint64_t *base) {
@@ -1588,6 +1639,16 @@ __global__ __launch_bounds__(1024) void dec_plan_kernel(DecArgs a, Ws ws)
         const uint64_t cap = m.status ? 0 : sym_cap(count, len);
         m.starts = m.slab + align_up(cap + 64, 16);
         m.csum = m.starts + 8 * group_entries_bound(a.out_caps[i]);
+        // the parallel boundary pass's data after the chunk sums: sub-chunk records, chunk
+        // records, Z entries, packed s0 (par_bytes)
+        const uint64_t nsub = par_subs(cap);
+        m.pcap = nsub != 0;
+        m.par = 0;
+        m.psub = align_up(m.csum + a.out_caps[i] / kChunk + 16, 16);
+        m.pchk = m.psub + align_up(sizeof(PSub) * nsub, 16);
+        m.pz = m.pchk + align_up(sizeof(PChk) * cdiv(nsub, kSubPerChunk), 16);
+        m.pzi = m.pz + align_up(4ull * kZcap * nsub, 16);
+        m.ps0 = m.pzi + align_up(4ull * kZcap * nsub, 16);
         ws.sym_offs[i] = m.sym;
         ws.sym_caps[i] = cap;
         ws.sym_lens[i] = 0;
@@ -1674,6 +1735,12 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
         }
         m.ents = m.mode == 0 ? cdiv(h, b) * cdiv(w, kTile) : m.groups;
         m.chunks = m.diff ? cdiv(w * h, kChunk) : 0;
+        // many block symbols: the parallel boundary pass (the slab holds its data, dec_plan)
+        m.par = m.pcap && nb && count - m.hdr >= par_min();
+        m.nsub = m.par ? cdiv(count - m.hdr, kSub) : 0;
+        m.nchk = cdiv(m.nsub, kSubPerChunk);
+        m.pfall = 0;
+        m.preruns = 0;
     };
     for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) parse(i);
     __syncthreads();
@@ -1681,16 +1748,18 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
         v[0] = ws.meta[i].status ? 0 : ws.meta[i].groups;
         v[1] = ws.meta[i].status ? 0 : ws.meta[i].chunks;
         v[2] = ws.meta[i].status ? 0 : ws.meta[i].tiles;
+        v[3] = ws.meta[i].status ? 0 : ws.meta[i].nsub;
     };
     auto put = [&](uint32_t i, const uint64_t *base) {
         ws.idx[0][i] = base[0];
         ws.idx[1][i] = base[1];
         ws.idx[2][i] = base[2];
+        ws.idx[3][i] = base[3];
     };
-    __shared__ uint64_t tot[3], uni[3];
-    wg_scan<3>(a.n, need, put, tot, uni);
+    __shared__ uint64_t tot[4], uni[4];
+    wg_scan<4>(a.n, need, put, tot, uni);
     if (threadIdx.x == 0) {
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < 4; ++k) {
             ws.idx[k][a.n] = tot[k];
             ws.ctr[k] = tot[k];
             ws.ctr[8 + k] = uni[k];
@@ -1729,78 +1798,190 @@ __device__ __forceinline__ uint32_t block_size(const AMeta &m, uint64_t k, uint6
     return 0;
 }
 
-// Where the blocks start (transform.cpp:330-361 running revertRLEBlock, transform.cpp:162-187,
-// block by block), reporting 13 / 14 / 15 exactly where the reference exits. One wave per
-// stream, 512 symbols per step (8 per lane, from dword loads re-aligned by v_alignbyte, the next
-// step's already in flight: a step always advances by 512 until the last block closes); a scan
-// of the transition functions gives each symbol's state, hence its output length (count: the
-// symbol, literal: 1); a scan of lengths finds the first symbol where the block's byte count is
-// reached. A block that ends inside the step re-scans the rest of the same registers from state
-// 0. The start of every K-th block is recorded for the unblock waves.
+// Block geometry of one adaptive stream (transform.cpp:25-62, 410-418): blocks in row-major
+// order, block row by starting at output offset by * B * W, block bx of it at bx * B * sy (sy
+// the row's height). 64-bit divisions by a double reciprocal, corrected (exact below 2^53).
+__device__ __forceinline__ uint64_t udiv(uint64_t a, uint64_t d, double inv)
+{
+    uint64_t q = (uint64_t)((double)a * inv);
+    uint64_t p = q * d;
+    while (p > a) {
+        --q;
+        p -= d;
+    }
+    while (a - p >= d) {
+        ++q;
+        p += d;
+    }
+    return q;
+}
+struct Geo {
+    uint64_t W, H, B, per_row, nbr, nb, RB, total;
+    double inv_RB;
+    __device__ void init(uint64_t w, uint64_t h, uint64_t b)
+    {
+        W = w;
+        H = h;
+        B = b;
+        per_row = cdiv(w, b);
+        nbr = cdiv(h, b);
+        nb = per_row * nbr;
+        RB = b * w;
+        total = w * h;
+        inv_RB = RB ? 1.0 / (double)RB : 0.0;
+    }
+    __device__ uint64_t sy(uint64_t by) const { return H - by * B < B ? H - by * B : B; }
+    __device__ uint64_t sx(uint64_t bx) const { return W - bx * B < B ? W - bx * B : B; }
+    // the block holding output offset o < total: (bx, by) and o - its first offset
+    __device__ void locate(uint64_t o, uint64_t &bx, uint64_t &by, uint64_t &rel) const
+    {
+        by = udiv(o, RB, inv_RB);
+        if (by >= nbr) by = nbr - 1;
+        const uint64_t r = o - by * RB, area = B * sy(by);
+        bx = udiv(r, area, 1.0 / (double)area);
+        if (bx >= per_row) bx = per_row - 1;
+        rel = r - bx * area;
+    }
+    // o is the first byte of a block
+    __device__ bool is_start(uint64_t o) const
+    {
+        if (o >= total) return false;
+        uint64_t bx, by, rel;
+        locate(o, bx, by, rel);
+        return rel == 0;
+    }
+};
+
+// The serial boundary process of one stream (transform.cpp:330-361 running revertRLEBlock,
+// transform.cpp:162-187, block by block), from any entry: symbols from `pos` in machine state r
+// at output offset E(blk) + got. One wave, 512 symbols per step (8 per lane, from dword loads
+// re-aligned by v_alignbyte, the next step's already in flight); a scan of the transition
+// functions gives each symbol's state, hence its output length (count: the symbol, literal: 1);
+// a scan of lengths finds the first symbol where the block's byte count is reached. A block that
+// ends inside the step re-scans the rest of the same registers from state 0. The start of every
+// K-th block (group) at or after `rec_from` is recorded for the unblock waves.
 #ifndef HC_BOUNDS_W
 #define HC_BOUNDS_W 2
 #endif
 constexpr uint32_t kBW = HC_BOUNDS_W;   // symbol dwords per lane and step
 constexpr uint32_t kBStep = 256 * kBW;  // symbols per step
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void bounds_kernel(DecArgs a, Ws ws)
-{
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-    for (uint32_t i = blockIdx.x * 4 + wv; i < a.n; i += gridDim.x * 4) {
-        AMeta &M = ws.meta[i];
-        if (M.status) continue;
-        const uint8_t *sym = at<uint8_t>(ws, M.sym);
-        uint64_t *starts = at<uint64_t>(ws, M.starts);
-        // the stream's parameters in registers (the starts[] stores could alias M's fields), and
-        // the current block's place stepped block by block (no 64-bit divisions per block)
-        const uint64_t W = M.w, H = M.h, B = M.B, K = M.K, ents = M.ents;
-        const bool tiled = M.mode == 0;
-        const uint64_t per_row = cdiv(W, B), ntx = cdiv(W, kTile);
-        uint64_t bx = 0, by = 0;   // block column / row of block blk
-        uint64_t kq = 0, gq = 0;   // mode 0: bx mod K, bx / K; else blk mod K, blk / K
-        auto block_want = [&]() -> uint64_t {
-            const uint64_t x0 = bx * B, y0 = by * B;
-            return (W - x0 < B ? W - x0 : B) * (H - y0 < B ? H - y0 : B);
-        };
-        // step to the next block; its group-start entry (~0 if it starts no group)
-        auto next_block = [&]() -> uint64_t {
-            if (++bx == per_row) {
-                bx = 0;
-                ++by;
-                if (tiled) kq = gq = 0;
-            } else if (tiled && ++kq == K) {
-                kq = 0;
-                ++gq;
-            }
-            if (!tiled && ++kq == K) {
-                kq = 0;
-                ++gq;
-            }
-            return kq ? ~0ull : (tiled ? by * ntx + gq : gq);
-        };
-        const uint64_t nsym = M.count, nb = M.nb;
-        // the dwords behind symbols p + kBStep * ... of lane `lane` (the slab is 16-aligned and
-        // holds 64 bytes of slack past the symbols; dwords starting past them read as 0)
-        const uint32_t *sw = reinterpret_cast<const uint32_t *>(sym);
-        auto load = [&](uint64_t p, uint32_t *w) {
-            const uint64_t d = (p >> 2) + kBW * lane;
+struct BWalk {
+    const uint32_t *sw;  // the stream's symbols as dwords (16-aligned slab, 64 bytes of slack)
+    uint64_t nsym;       // symbols (adaptive header included)
+    uint64_t hdr;        // first block symbol
+    uint64_t *starts;
+    uint64_t K, ents, ntx;
+    bool tiled;
+    uint64_t W, H, B, per_row, nb;  // geometry (Geo geo() for the rest: entries and exits only)
+    uint32_t lane;
+    // process state
+    uint64_t pos, blk, got, want;
+    uint64_t bx, by, kq, gq;  // block column / row; mode 0: bx mod K, bx / K; else blk mod K, blk / K
+    uint32_t r, last;
+
+    __device__ void init(const AMeta &M, const uint8_t *sym, uint64_t *st, uint32_t l)
+    {
+        sw = reinterpret_cast<const uint32_t *>(sym);
+        nsym = M.count;
+        hdr = M.hdr;
+        starts = st;
+        K = M.K;
+        ents = M.ents;
+        tiled = M.mode == 0;
+        W = M.w;
+        H = M.h;
+        B = M.B;
+        per_row = cdiv(W, B);
+        nb = per_row * cdiv(H, B);
+        ntx = cdiv(M.w, kTile);
+        lane = l;
+    }
+    __device__ Geo geo() const
+    {
+        Geo g;
+        g.init(W, H, B);
+        return g;
+    }
+    __device__ uint64_t block_want() const
+    {
+        return (W - bx * B < B ? W - bx * B : B) * (H - by * B < B ? H - by * B : B);
+    }
+    __device__ uint64_t entry() const { return tiled ? by * ntx + gq : gq; }  // when kq == 0
+    // step to the next block; its group-start entry (~0 if it starts no group)
+    __device__ uint64_t next_block()
+    {
+        if (++bx == per_row) {
+            bx = 0;
+            ++by;
+            if (tiled) kq = gq = 0;
+        } else if (tiled && ++kq == K) {
+            kq = 0;
+            ++gq;
+        }
+        if (!tiled && ++kq == K) {
+            kq = 0;
+            ++gq;
+        }
+        return kq ? ~0ull : entry();
+    }
+    // output offset of the process: the current block's first byte + got
+    __device__ uint64_t offset() const
+    {
+        return blk >= nb ? W * H : by * B * W + bx * B * (H - by * B < B ? H - by * B : B) + got;
+    }
+    // enter at symbol q in state r0 at output offset o (a block start resets the state)
+    __device__ void enter(uint64_t q, uint32_t r0, uint64_t o, uint64_t rec_from)
+    {
+        pos = q;
+        r = r0;
+        last = q > hdr ? reinterpret_cast<const uint8_t *>(sw)[q - 1] : 0u;
+        got = 0;
+        if (o >= W * H) {
+            blk = nb;
+            bx = by = kq = gq = 0;
+            want = 0;
+            return;
+        }
+        uint64_t rel;
+        geo().locate(o, bx, by, rel);
+        blk = by * per_row + bx;
+        got = rel;
+        want = block_want();
+        if (tiled) {
+            kq = bx % K;
+            gq = bx / K;
+        } else {
+            kq = blk % K;
+            gq = blk / K;
+        }
+        if (got == 0) {
+            r = 0;
+            if (kq == 0 && q >= rec_from && lane == 0 && entry() < ents) starts[entry()] = q;
+        }
+    }
+    __device__ void load(uint64_t p, uint32_t *w) const
+    {
+        const uint64_t d = (p >> 2) + kBW * lane;
 #pragma unroll
-            for (uint32_t j = 0; j <= kBW; ++j) w[j] = 4 * (d + j) < nsym ? sw[d + j] : 0u;
-        };
-        uint64_t pos = M.hdr;
-        uint64_t blk = 0, got = 0;
-        uint32_t r = 0, last = 0;
-        int status = 0;
-        if (lane == 0 && nb) starts[0] = pos;
-        uint64_t want = nb ? block_want() : 0;
+        for (uint32_t j = 0; j <= kBW; ++j) w[j] = 4 * (d + j) < nsym ? sw[d + j] : 0u;
+    }
+    // run over the symbols below q1 (<= nsym): 0 when q1 is reached with blocks left, or the
+    // reference's exit there: 13 (a count overshoots its block), 14 (the stream ends inside a
+    // block), 15 (symbols left after the last block); blk == nb with pos == nsym: 0 (done)
+    // kWhole: the whole stream from its start (q1 = nsym, every start recorded)
+    template <bool kWhole = false>
+    __device__ int run(uint64_t q1, uint64_t rec_from)
+    {
+        if constexpr (kWhole) {
+            q1 = nsym;
+            rec_from = 0;
+        }
         uint32_t cur[kBW + 1];
         load(pos, cur);
         while (blk < nb) {
-            const uint64_t avail = nsym - pos;
+            const uint64_t avail = q1 - pos;
             const uint32_t m = avail < kBStep ? (uint32_t)avail : kBStep;
-            if (m == 0) {  // transform.cpp:170-174: the block wants more, the stream is empty
-                status = HC_ERR_BLOCK_EOF;
-                break;
-            }
+            if (m == 0) return pos == nsym ? HC_ERR_BLOCK_EOF : 0;  // transform.cpp:170-174
             uint32_t nxt[kBW + 1];
             load(pos + kBStep, nxt);  // the next step's symbols, in flight during this one
             constexpr uint32_t kB = 4 * kBW;
@@ -1813,7 +1994,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void b
             }
             const uint32_t up = lane_shr1(x[kB - 1], last);
             uint32_t lo = 0;  // symbols below lo belong to blocks already closed
-            bool stop = false;
             for (;;) {
                 uint32_t f[kB], F = kFsmId;
 #pragma unroll
@@ -1858,33 +2038,755 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void b
                 }
                 j = readlane(j, L);
                 cj = readlane(cj, L);
-                if ((uint64_t)cj != need) {  // transform.cpp:178-182: a count overshoots the block
-                    status = HC_ERR_BLOCK_DATA;
-                    stop = true;
-                    break;
-                }
+                if ((uint64_t)cj != need) return HC_ERR_BLOCK_DATA;  // transform.cpp:178-182
                 lo = j + 1;
                 ++blk;
                 const uint64_t e = next_block();
-                if (blk < nb && lane == 0 && e < ents) starts[e] = pos + lo;  // (e = ~0: no group start)
+                if (blk < nb && lane == 0 && e < ents && pos + lo >= rec_from) starts[e] = pos + lo;
+                // the next block starts in state 0 (the previous symbol does not matter then; at a
+                // chunk exit on a block end the state is not compared either: par_fix)
+                r = 0;
+                got = 0;
                 if (blk == nb) {
                     pos += lo;
-                    break;
+                    return pos != nsym ? HC_ERR_LEFTOVER : 0;  // transform.cpp:354-358
                 }
                 want = block_want();
-                got = 0;
-                r = 0;
-                if (lo == m) {
+                if (lo == m) {  // the block ends with the step: the next starts at pos + m
                     pos += m;
                     break;
                 }
             }
-            if (stop) break;
 #pragma unroll
             for (uint32_t j = 0; j <= kBW; ++j) cur[j] = nxt[j];
         }
-        if (status == 0 && pos != nsym) status = HC_ERR_LEFTOVER;  // transform.cpp:354-358
+        return pos != nsym ? HC_ERR_LEFTOVER : 0;
+    }
+};
+
+// One wave per stream (the streams the parallel pass below does not take): the serial process
+// over the whole stream.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void bounds_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    for (uint32_t i = blockIdx.x * 4 + wv; i < a.n; i += gridDim.x * 4) {
+        AMeta &M = ws.meta[i];
+        if (M.status || M.par) continue;
+        BWalk w;
+        w.init(M, at<uint8_t>(ws, M.sym), at<uint64_t>(ws, M.starts), lane);
+        // the stream's start: block 0 in state 0
+        w.pos = M.hdr;
+        w.r = w.last = 0;
+        w.blk = w.got = w.bx = w.by = w.kq = w.gq = 0;
+        w.want = w.block_want();
+        if (lane == 0 && w.nb) w.starts[0] = M.hdr;
+        const int status = w.run<true>(0, 0);
         if (lane == 0) M.status = status;
+    }
+}
+
+// ------------------------------------------------------ parallel block-boundary pass ------
+// For a stream of many symbols (C4: 11 M), the serial process above is one wave's chain of
+// block ends. The parallel pass (model and argument: tests/bounds_par_model.py):
+//   par_fsm    per 2048-symbol sub-chunk: the composed transition function of its symbols;
+//   par_entry  per stream: a scan of those: the no-reset machine's state s0 at each sub-chunk;
+//   par_z      per sub-chunk: s0, lengths and offsets of every symbol without block resets
+//              (packed s0 kept), and Z: the symbols where a reset (a block start) would change
+//              some length before the reset machine rejoins s0;
+//   par_scan   per stream, one wave: Z in order with the running correction D: z is a block
+//              start iff O0(z) + D is a block's first byte; there the true machine runs until it
+//              rejoins s0 (new D). Writes each 16384-symbol chunk's predicted entry;
+//   par_walk   per chunk: the serial process from its predicted entry: block starts, error,
+//              exit;
+//   par_fix    per stream: entries checked against the previous chunk's exit in order, chunks
+//              that differ re-run from the exact exit (so the result is exact whatever par_scan
+//              predicted); the first error is the stream's status.
+__device__ __forceinline__ uint32_t fsm_step(uint32_t x, uint32_t xp) { return x == xp ? kFsmEq : kFsmNe; }
+
+// symbols p0 + 32 lane .. + 31 (< end) as 8 dwords per lane (bytes past end: 0); returns the
+// symbol before the lane's first (lane 0: before p0, 0 at the block data start)
+__device__ __forceinline__ uint32_t load_sub(const uint8_t *sym, uint64_t hdr, uint64_t p0, uint64_t end, uint32_t lane,
+                                             uint32_t *w)
+{
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(sym);
+    const uint64_t b = p0 + 32 * lane;
+    const uint64_t d = b >> 2;
+    uint32_t raw[9];
+#pragma unroll
+    for (uint32_t j = 0; j < 9; ++j) raw[j] = 4 * (d + j) < end + 4 ? sw[d + j] : 0u;  // (slab slack)
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        uint32_t v = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], (uint32_t)(b & 3));
+        const uint64_t q = b + 4 * j;  // mask bytes at or past end
+        if (q + 4 > end) v = q >= end ? 0u : (v & (0xFFFFFFFFu >> (8 * (uint32_t)(q + 4 - end))));
+        w[j] = v;
+    }
+    const uint32_t prev_lane = lane_shr1(w[7] >> 24, 0u);
+    const uint32_t before = p0 > hdr ? (uint32_t)sym[p0 - 1] : 0u;
+    return lane == 0 ? before : prev_lane;
+}
+// the lane's 32 symbols' composed transition function (symbols at or past end: identity)
+__device__ __forceinline__ uint32_t lane_fsm(const uint32_t *w, uint32_t prev, uint64_t p, uint64_t end)
+{
+    uint32_t F = kFsmId, xp = prev;
+#pragma unroll
+    for (uint32_t t = 0; t < 32; ++t) {
+        const uint32_t x = (w[t >> 2] >> (8 * (t & 3))) & 255u;
+        F = p + t < end ? fsm_then(fsm_step(x, xp), F) : F;
+        xp = x;
+    }
+    return F;
+}
+
+// per-stream data of the pass, in the stream's slab
+__device__ __forceinline__ PSub *psub(const Ws &ws, const AMeta &M) { return at<PSub>(ws, M.psub); }
+__device__ __forceinline__ PChk *pchk(const Ws &ws, const AMeta &M) { return at<PChk>(ws, M.pchk); }
+
+// the sub-chunk of work item t: stream i, sub j
+__device__ __forceinline__ bool sub_item(const DecArgs &a, const Ws &ws, uint64_t t, uint32_t &i, uint64_t &j)
+{
+    i = find_item(ws.idx[3], a.n, t, ws.ctr[8 + 3]);
+    const AMeta &M = ws.meta[i];
+    j = t - ws.idx[3][i];
+    return M.status == 0 && M.par && j < M.nsub;
+}
+
+__global__ __launch_bounds__(256) void par_fsm_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t items = ws.ctr[3];
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
+        uint32_t i;
+        uint64_t j;
+        if (!sub_item(a, ws, t, i, j)) continue;
+        const AMeta &M = ws.meta[i];
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        const uint64_t p0 = M.hdr + j * kSub, end = p0 + kSub < M.count ? p0 + kSub : M.count;
+        uint32_t w[8];
+        const uint32_t prev = load_sub(sym, M.hdr, p0, end, lane, w);
+        const uint32_t F = fsm_scan(lane_fsm(w, prev, p0 + 32 * lane, end));
+        if (lane == 63) psub(ws, M)[j].F = F;
+    }
+}
+
+// one wave per stream: s0 at every sub-chunk (the machine starts in state 0 at the block data)
+__global__ __launch_bounds__(64) void par_entry_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id();
+    for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+        const AMeta &M = ws.meta[i];
+        if (M.status || !M.par) continue;
+        PSub *S = psub(ws, M);
+        uint32_t carry = 0;
+        for (uint64_t b = 0; b < M.nsub; b += 64) {
+            const bool ok = b + lane < M.nsub;
+            const uint32_t f = ok ? S[b + lane].F : kFsmId;
+            const uint32_t inc = fsm_scan(f);
+            if (ok) S[b + lane].s0 = fsm_at(lane_shr1(inc, kFsmId), carry);
+            carry = fsm_at(readlane(inc, 63), carry);
+        }
+    }
+}
+
+// per sub-chunk: packed s0 (2 bits per symbol), no-reset bytes L, and the Z entries
+// (offset in the sub-chunk's no-reset output << 11 | symbol index in the sub-chunk)
+__global__ __launch_bounds__(256) void par_z_kernel(DecArgs a, Ws ws)
+{
+    __shared__ uint8_t X[4][kSub + kWinLook + 4];  // symbols p0 - 4 .. end + kWinLook
+    __shared__ uint8_t S0[4][kSub + kWinLook];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t items = ws.ctr[3];
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
+        uint32_t i;
+        uint64_t j;
+        if (!sub_item(a, ws, t, i, j)) continue;
+        const AMeta &M = ws.meta[i];
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        PSub *SB = psub(ws, M);
+        const uint64_t n = M.count;
+        const uint64_t p0 = M.hdr + j * kSub, end = p0 + kSub < n ? p0 + kSub : n;
+        const uint32_t cnt = (uint32_t)(end - p0);
+        uint32_t w[8];
+        const uint32_t prev = load_sub(sym, M.hdr, p0, end, lane, w);
+        const uint32_t Fl = lane_fsm(w, prev, p0 + 32 * lane, end);
+        const uint32_t inc = fsm_scan(Fl);
+        uint32_t s = fsm_at(lane_shr1(inc, kFsmId), SB[j].s0);  // no-reset state at the lane's first
+        uint8_t *Xw = X[wv] + 4, *Sw = S0[wv];
+        // per symbol: s0 (packed and in LDS), no-reset length
+        uint32_t pk0 = 0, pk1 = 0, lsum = 0, xp = prev;
+#pragma unroll
+        for (uint32_t k = 0; k < 32; ++k) {
+            const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 255u;
+            const bool ok = 32 * lane + k < cnt;
+            if (k < 16) pk0 |= s << (2 * k);
+            else pk1 |= s << (2 * (k - 16));
+            Xw[32 * lane + k] = (uint8_t)x;
+            Sw[32 * lane + k] = (uint8_t)s;
+            lsum += ok ? (s == 3 ? x : 1u) : 0u;
+            s = ok ? fsm_at(fsm_step(x, xp), s) : s;
+            xp = x;
+        }
+        if (lane == 0) Xw[-1] = (uint8_t)prev;
+        uint32_t *pk = at<uint32_t>(ws, M.ps0) + j * (kSub / 16);
+        pk[2 * lane] = pk0;
+        pk[2 * lane + 1] = pk1;
+        // lookahead: the next sub-chunk's first kWinLook symbols and their s0
+        {
+            const uint64_t q = end + lane;
+            const uint32_t x = q < n ? sym[q] : 0u;
+            const uint32_t xq = lane_shr1(x, cnt ? (uint32_t)sym[end - 1] : 0u);
+            const uint32_t f = q < n ? fsm_step(x, xq) : kFsmId;
+            const uint32_t sc = end < n ? SB[j + 1].s0 : 0u;
+            const uint32_t li = fsm_scan(f);
+            Xw[cnt + lane] = (uint8_t)x;
+            Sw[cnt + lane] = (uint8_t)fsm_at(lane_shr1(li, kFsmId), sc);
+        }
+        const uint32_t lacc = wave_sum_incl(lsum);
+        const uint32_t obase = lacc - lsum;  // no-reset output before the lane's first symbol
+        if (lane == 63) SB[j].L = lacc;
+        __builtin_amdgcn_wave_barrier();
+        // Z: from each symbol p, the machine reset to 0 there, until it rejoins s0 (at most
+        // kWinLook symbols; a window that does not rejoin counts as Z: the scanner simulates it)
+        uint32_t zmask = 0;
+        const uint32_t lim = cnt + kWinLook < (uint32_t)(n - p0) ? cnt + kWinLook : (uint32_t)(n - p0);
+        // the machine reset to 0 at symbol p, until it rejoins s0: whether a length differs (Z),
+        // and for the scanner's fast path (zinfo) the window's length, its length correction
+        // and its output without the last symbol (0: no fast path)
+        auto window = [&](uint32_t p, uint32_t &info) __attribute__((always_inline)) -> bool {
+            uint32_t u = 0, q = p, wt = 0, lt = 0;
+            int32_t dl = 0;
+            bool mism = false;
+            while (q < lim && u != Sw[q] && q - p < kWinLook) {
+                const uint32_t x = Xw[q], s0q = Sw[q];
+                lt = u == 3 ? x : 1u;
+                const uint32_t l0 = s0q == 3 ? x : 1u;
+                mism |= lt != l0;
+                dl += (int32_t)lt - (int32_t)l0;
+                wt += lt;
+                u = fsm_at(fsm_step(x, Xw[(int)q - 1]), u);
+                ++q;
+            }
+            const bool synced = q < lim ? u == Sw[q] : false;
+            const uint32_t wl = q - p, wo = wt - lt;
+            info = synced && wl < 64 && dl >= -4096 && dl < 4096 && wo < 8192
+                       ? wl | ((uint32_t)(dl + 4096) << 6) | (wo << 19) : 0u;
+            return mism || (q < lim && !synced);
+        };
+        for (uint32_t k = 0; k < 32; ++k) {
+            const uint32_t p = 32 * lane + k;
+            if (p >= cnt) break;
+            uint32_t info;
+            if (window(p, info)) zmask |= 1u << k;
+        }
+        const uint32_t zc = (uint32_t)__builtin_popcount(zmask);
+        const uint32_t zacc = wave_sum_incl(zc);
+        const uint32_t ztot = readlane(zacc, 63);
+        if (ztot <= kZcap) {
+            uint32_t *Z = at<uint32_t>(ws, M.pz) + j * kZcap;
+            uint32_t *ZI = at<uint32_t>(ws, M.pzi) + j * kZcap;
+            uint32_t at_ = zacc - zc;
+            uint32_t oo = obase;
+            for (uint32_t k = 0; k < 32; ++k) {
+                const uint32_t p = 32 * lane + k;
+                if (p >= cnt) break;
+                if ((zmask >> k) & 1u) {
+                    uint32_t info;
+                    (void)window(p, info);
+                    ZI[at_] = info;
+                    Z[at_++] = (oo << 11) | p;
+                }
+                const uint32_t s0p = Sw[p], x = Xw[p];
+                oo += s0p == 3 ? x : 1u;
+            }
+        }
+        if (lane == 0) SB[j].zn = ztot <= kZcap ? ztot : kDense;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// the no-reset state s0 of symbol p (packed by par_z)
+__device__ __forceinline__ uint32_t s0_at(const uint32_t *pk, uint64_t rel)
+{
+    return (pk[rel >> 4] >> (2 * (rel & 15))) & 3u;
+}
+
+// One workgroup per stream: Z in order with the running correction D
+// (tests/bounds_par_model.py). The serial part -- D changes at every block start found in Z --
+// is one wave (the consumer); the other 15 (producers) run up to kRing sub-chunks ahead of it:
+// each loads a sub-chunk's record, Z entries and window infos into an LDS ring slot and tests
+// them against the D the consumer last published (a version of it), noting the first candidate
+// and loading the symbols around it. The consumer takes a slot whose test used the current
+// version as it is (no candidate: nothing to do), and tests it again otherwise (after a block
+// start found since). A block start in Z whose window par_z could describe (not split by a block
+// end or a chunk start) takes D += its correction at once; any other is simulated symbol by
+// symbol, from the slot's prefetched window when it is that one.
+constexpr uint32_t kZr = kZcap / 64;  // Z entries per lane and sub-chunk
+constexpr uint32_t kRing = 12;        // ring slots (sub-chunks ahead of the consumer)
+constexpr uint32_t kSpinCap = 1u << 23;  // sleeps before a wait gives up (~1 s; never expected)
+constexpr uint32_t kProd = 11;        // producer waves (12 waves per workgroup: registers for the consumer's paths)
+struct RSlot {
+    uint32_t j;      // the sub-chunk published here (0xFFFFFFFF: none yet)
+    uint32_t ver;    // the D version its test used
+    uint32_t first;  // first candidate under that version: entry index (dense: symbol index), ~0 none
+    uint32_t zn;     // entries (kDense: dense, no entries here)
+    uint32_t s0, L;
+    uint64_t o0;
+    uint64_t wz;     // the prefetched window's block start (~0: none)
+    uint32_t wx[16];  // symbols wz - 1 .. wz + 62
+    uint32_t ws[4];   // s0 of wz .. wz + 63: bit planes (low 64 bits, high 64 bits)
+    uint32_t ze[kZcap], zi[kZcap];
+};
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
+
+__global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, Ws ws)
+{
+    __shared__ RSlot ring[kRing];
+    __shared__ uint32_t OD[kSub];            // consumer: a dense sub-chunk's no-reset offsets
+    __shared__ int64_t vD[64];                // D of version v at [v % 64]
+    __shared__ uint64_t vres[64];             // resume of version v
+    __shared__ uint32_t sh_ver, sh_done, sh_quit;
+    __shared__ uint32_t part[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+        AMeta &M = ws.meta[i];
+        if (M.status || !M.par) continue;  // (uniform over the workgroup)
+        const uint8_t *sym = at<uint8_t>(ws, M.sym);
+        const uint32_t *pk = at<uint32_t>(ws, M.ps0);
+        PSub *SB = psub(ws, M);
+        PChk *C = pchk(ws, M);
+        const uint32_t *Zall = at<uint32_t>(ws, M.pz), *ZIall = at<uint32_t>(ws, M.pzi);
+        Geo g;
+        g.init(M.w, M.h, M.B);
+        const uint64_t n = M.count, hdr = M.hdr, nsub = M.nsub;
+        const uint64_t span = (uint64_t)kSub * kSubPerChunk;
+        // fast test: below full_end every block start is a multiple of B^2 (mask = B^2 - 1) and
+        // every block holds B^2 bytes
+        const bool pow2 = (g.B & (g.B - 1)) == 0 && g.W % g.B == 0 && g.B <= 4096;
+        const uint64_t mask = pow2 ? g.B * g.B - 1 : 0, full_end = pow2 ? (g.nbr - 1) * g.RB : 0;
+        // 1. the no-reset offset of every sub-chunk (exclusive scan of L, the whole workgroup)
+        {
+            uint64_t carry = 0;
+            constexpr uint32_t kT = 64 * (kProd + 1);
+            for (uint64_t b = 0; b < nsub; b += kT) {
+                const uint64_t j = b + tid;
+                const uint32_t l = j < nsub ? SB[j].L : 0u;
+                const uint32_t inc = wave_sum_incl(l);
+                if (lane == 63) part[wv] = inc;
+                __syncthreads();
+                uint64_t before = carry, tot = 0;
+                for (uint32_t w = 0; w < kProd + 1; ++w) {
+                    before += w < wv ? part[w] : 0u;
+                    tot += part[w];
+                }
+                if (j < nsub) SB[j].o0 = before + inc - l;
+                carry += tot;
+                __syncthreads();
+            }
+        }
+        if (tid < kRing) ring[tid].j = 0xFFFFFFFFu;
+        if (tid == 0) {
+            sh_ver = 0;
+            sh_done = 0;
+            sh_quit = 0;
+            vD[0] = 0;
+            vres[0] = 0;
+        }
+        __syncthreads();  // (also makes the o0 stores visible to the workgroup)
+        // the block-start test of entry e (rel << 11 | symbol index) of a sub-chunk at p0 with
+        // no-reset offset o0, under (D, resume)
+        auto test = [&](uint32_t e, bool ok, uint64_t p0, uint64_t o0, int64_t D, uint64_t resume)
+            __attribute__((always_inline)) -> bool {
+            const uint64_t base = o0 + D;
+            const uint32_t rres = resume <= p0 ? 0u : (resume - p0 >= kSub ? kSub : (uint32_t)(resume - p0));
+            const uint32_t bm = (uint32_t)(base & mask);
+            const uint32_t rlim =
+                base >= full_end ? 0u : (full_end - base > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(full_end - base));
+            const uint32_t pr = e & 2047u, rel = e >> 11;
+            bool hit;
+            if (rel < rlim) hit = ((bm + rel) & (uint32_t)mask) == 0;
+            else hit = ok && g.is_start(base + rel);
+            return ok && pr >= rres && hit;
+        };
+        // dense sub-chunk j: each of this lane's 32 symbols (32 lane + q) with its no-reset offset in
+        // the sub-chunk, handed to f(q, offset) in order (two passes over the loaded symbols: no
+        // per-symbol arrays)
+        auto dense_each = [&](uint64_t j, uint64_t p0, uint32_t cnt, auto f) __attribute__((always_inline)) {
+            uint32_t w[8];
+            (void)load_sub(sym, hdr, p0, p0 + cnt, lane, w);
+            const uint32_t s0lo = pk[j * (kSub / 16) + 2 * lane], s0hi = pk[j * (kSub / 16) + 2 * lane + 1];
+            auto len = [&](uint32_t q) __attribute__((always_inline)) {
+                const uint32_t x = (w[q >> 2] >> (8 * (q & 3))) & 255u;
+                const uint32_t s0 = ((q < 16 ? s0lo : s0hi) >> (2 * (q & 15))) & 3u;
+                return 32 * lane + q < cnt ? (s0 == 3 ? x : 1u) : 0u;
+            };
+            uint32_t tot = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 32; ++q) tot += len(q);
+            const uint32_t inc = wave_sum_incl(tot);
+            uint32_t acc = inc - tot;
+#pragma unroll
+            for (uint32_t q = 0; q < 32; ++q) {
+                f(q, acc);
+                acc += len(q);
+            }
+        };
+        if (wv > 0) {
+            // ------------------------------------------------------------- producers
+            for (uint64_t j = wv - 1; j < nsub; j += kProd) {
+                RSlot &R = ring[j % kRing];
+                // the slot is free once the consumer is done with sub-chunk j - kRing (bounded: a
+                // wait past ~1 s gives up, and the serial pass in par_fix takes over)
+                for (uint32_t spin = 0; lds_ld(&sh_done) + kRing <= j && !lds_ld(&sh_quit); ++spin) {
+                    if (spin > kSpinCap) {
+                        lds_st(&sh_quit, 2u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (lds_ld(&sh_quit)) break;
+                const PSub rec = SB[j];
+                const uint64_t p0 = hdr + j * kSub;
+                const uint32_t cnt = (uint32_t)((p0 + kSub < n ? p0 + kSub : n) - p0);
+                const bool dense = rec.zn == kDense;
+                uint32_t e[kZr], zi[kZr];
+                if (!dense) {
+#pragma unroll
+                    for (uint32_t r = 0; r < kZr; ++r) {
+                        const uint32_t it = 64 * r + lane;
+                        e[r] = it < rec.zn ? Zall[j * kZcap + it] : 0xFFFFFFFFu;
+                        zi[r] = it < rec.zn ? ZIall[j * kZcap + it] : 0u;
+                    }
+                }
+                // the consumer's current version of (D, resume)
+                const uint32_t v = lds_ld(&sh_ver);
+                const int64_t D = vD[v % 64];
+                const uint64_t resume = vres[v % 64];
+                uint32_t first = 0xFFFFFFFFu;
+                if (!dense) {
+#pragma unroll
+                    for (int r = kZr - 1; r >= 0; --r) {
+                        const uint64_t m = ballot(test(e[r], e[r] != 0xFFFFFFFFu, p0, rec.o0, D, resume));
+                        if (m) first = 64 * r + (uint32_t)__builtin_ctzll(m);
+                    }
+#pragma unroll
+                    for (uint32_t r = 0; r < kZr; ++r) {
+                        R.ze[64 * r + lane] = e[r];
+                        R.zi[64 * r + lane] = zi[r];
+                    }
+                } else {
+                    uint64_t any = 0;
+                    uint32_t fq = 0xFFFFFFFFu;
+                    dense_each(j, p0, cnt, [&](uint32_t q, uint32_t od) __attribute__((always_inline)) {
+                        const bool h = test((od << 11) | (32 * lane + q), 32 * lane + q < cnt, p0, rec.o0, D, resume);
+                        fq = h && fq == 0xFFFFFFFFu ? 32 * lane + q : fq;
+                    });
+                    any = ballot(fq != 0xFFFFFFFFu);
+                    if (any) first = readlane(fq, (uint32_t)__builtin_ctzll(any));  // lanes hold ascending symbols
+                }
+                // the window around the first candidate: symbols z - 1 .. z + 62, s0 of z .. z + 63
+                uint64_t wz = ~0ull;
+                if (first != 0xFFFFFFFFu) {
+                    const uint32_t ef = dense ? first : (readlane(e[0], first & 63) & 2047u);
+                    uint32_t efr = e[0];
+#pragma unroll
+                    for (uint32_t r = 1; r < kZr; ++r) efr = (first >> 6) == r ? e[r] : efr;
+                    wz = p0 + (dense ? ef : (readlane(efr, first & 63) & 2047u));
+                    const uint64_t pl = wz + lane;
+                    const uint32_t x = pl - 1 < n ? sym[pl - 1] : 0u;
+                    const uint32_t s0q = pl < n ? s0_at(pk, pl - hdr) : 0u;
+                    reinterpret_cast<uint8_t *>(R.wx)[lane] = (uint8_t)x;
+                    const uint64_t b0 = ballot(s0q & 1u), b1 = ballot(s0q & 2u);
+                    if (lane == 0) {
+                        R.ws[0] = (uint32_t)b0;
+                        R.ws[1] = (uint32_t)(b0 >> 32);
+                        R.ws[2] = (uint32_t)b1;
+                        R.ws[3] = (uint32_t)(b1 >> 32);
+                    }
+                }
+                if (lane == 0) {
+                    R.ver = v;
+                    R.first = first;
+                    R.zn = rec.zn;
+                    R.s0 = rec.s0;
+                    R.L = rec.L;
+                    R.o0 = rec.o0;
+                    R.wz = wz;
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot's LDS writes are done
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) lds_st(&R.j, (uint32_t)j);  // published
+            }
+        } else {
+            // -------------------------------------------------------------- consumer
+            int64_t D = 0;         // true offset - no-reset offset, outside the windows
+            uint64_t resume = 0;   // symbols below this are inside a window already done
+            uint32_t ver = 0;
+            uint64_t next_chunk = 0;
+            bool stop = false;     // an error or the end inside a window: the walks report it
+            uint32_t fall = 0;
+            auto publish = [&]() __attribute__((always_inline)) {
+                ++ver;
+                if (lane == 0) {
+                    vD[ver % 64] = D;
+                    vres[ver % 64] = resume;
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) lds_st(&sh_ver, ver);
+            };
+            for (uint64_t j = 0; j < nsub && !stop; ++j) {
+                RSlot &R = ring[j % kRing];
+                for (uint32_t spin = 0; lds_ld(&R.j) != (uint32_t)j; ++spin) {
+                    if (lds_ld(&sh_quit) || spin > kSpinCap) {  // (a producer gave up: never expected)
+                        fall = 1;
+                        stop = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (stop) break;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const uint64_t p0 = hdr + j * kSub;
+                const uint64_t o0 = R.o0;
+                const uint32_t zn = R.zn, rv = R.ver, rfirst = R.first;
+                if (j % kSubPerChunk == 0 && j / kSubPerChunk >= next_chunk) {
+                    const uint64_t c = j / kSubPerChunk;
+                    if (lane == 0) {
+                        C[c].q0 = p0;
+                        C[c].o_in = o0 + D;
+                        C[c].r_in = R.s0;
+                    }
+                    next_chunk = c + 1;
+                }
+                const bool dense = zn == kDense;
+                const uint32_t cnt = (uint32_t)((p0 + kSub < n ? p0 + kSub : n) - p0);
+                const uint32_t items = dense ? cnt : zn;
+                // the producer's test holds while no block start was found since it ran
+                if (!(rv == ver && rfirst == 0xFFFFFFFFu)) {
+                    if (dense) {
+                        dense_each(j, p0, cnt, [&](uint32_t q, uint32_t od) __attribute__((always_inline)) {
+                            OD[32 * lane + q] = od;
+                        });
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                    const uint32_t b_first = rv == ver ? (rfirst & ~63u) : 0u;
+                    for (uint32_t b = b_first; b < items && !stop; b += 64) {
+                        const bool ok = b + lane < items;
+                        const uint32_t e = ok ? (dense ? (OD[b + lane] << 11) | (b + lane) : R.ze[b + lane]) : 0xFFFFFFFFu;
+                        uint64_t cand = ballot(test(e, ok, p0, o0, D, resume));
+                        while (cand && !stop) {
+                            const uint32_t L = (uint32_t)__builtin_ctzll(cand);
+                            const uint32_t eL = readlane(e, L);
+                            const uint32_t ziL = dense ? 0u : R.zi[b + L];
+                            const uint64_t z = p0 + (eL & 2047u);
+                            const uint64_t oz0 = o0 + (eL >> 11);  // O0(z)
+                            const uint64_t o = oz0 + D;
+                            // fast path: the window par_z described, inside one block (B^2 bytes),
+                            // no chunk start inside it
+                            const uint32_t wl = ziL & 63u, wo = ziL >> 19;
+                            const uint64_t cz = (z - hdr) / span, cw = (z + wl - 1 - hdr) / span;
+                            if (ziL && o < full_end && mask + 1 > wo && cz == cw) {
+                                D += (int64_t)((ziL >> 6) & 8191u) - 4096;
+                                resume = z + wl;
+                                publish();
+                                cand = ballot(test(e, ok, p0, o0, D, resume));
+                                continue;
+                            }
+                            // the true machine from the block start z until it rejoins s0; the
+                            // window from the slot when the producer prefetched this one
+                            uint64_t ot = o, o0t = oz0, got = 0, want;
+                            uint64_t bx, by, rl;
+                            g.locate(ot, bx, by, rl);
+                            want = g.sx(bx) * g.sy(by);
+                            uint64_t blk = by * g.per_row + bx;
+                            uint32_t u = 0;
+                            uint64_t q = z;
+                            uint32_t xw = 0, sw0 = 0;  // window: symbols q - 1 + lane, s0 of q + lane
+                            uint64_t wbase = ~0ull;
+                            if (R.wz == z) {
+                                wbase = z;
+                                xw = reinterpret_cast<const uint8_t *>(R.wx)[lane];
+                                const uint64_t p0l = (uint64_t)R.ws[1] << 32 | R.ws[0], p1l = (uint64_t)R.ws[3] << 32 | R.ws[2];
+                                sw0 = (uint32_t)((p0l >> lane) & 1u) | (uint32_t)(((p1l >> lane) & 1u) << 1);
+                            }
+                            for (;;) {
+                                if (q > z && got == 0) u = 0;  // a block start inside the window
+                                if (q >= n) {
+                                    stop = true;
+                                    break;
+                                }
+                                if (q - z >= kWinCap) {
+                                    fall = 1;
+                                    stop = true;
+                                    break;
+                                }
+                                if (wbase == ~0ull || q - wbase >= 63) {  // (re)load the window at q
+                                    wbase = q;
+                                    const uint64_t pl = q + lane;
+                                    xw = pl - 1 < n ? sym[pl - 1] : 0u;
+                                    sw0 = pl < n ? s0_at(pk, pl - hdr) : 0u;
+                                }
+                                const uint32_t s0q = readlane(sw0, (uint32_t)(q - wbase));
+                                if (q > z && u == s0q) break;  // rejoined
+                                if ((q - hdr) % span == 0 && q > z) {
+                                    // a chunk start inside the window: its walk runs in from z
+                                    const uint64_t c = (q - hdr) / span;
+                                    if (lane == 0) {
+                                        C[c].q0 = z;
+                                        C[c].o_in = oz0 + D;
+                                        C[c].r_in = 0;
+                                    }
+                                    next_chunk = c + 1;
+                                }
+                                const uint32_t x = readlane(xw, (uint32_t)(q - wbase) + 1);
+                                const uint32_t xp = readlane(xw, (uint32_t)(q - wbase));
+                                const uint32_t lt = u == 3 ? x : 1u;
+                                o0t += s0q == 3 ? x : 1u;
+                                ot += lt;
+                                got += lt;
+                                u = fsm_at(fsm_step(x, xp), u);
+                                ++q;
+                                if (got > want) {  // overshoot: status 13, reported by the walks
+                                    stop = true;
+                                    break;
+                                }
+                                if (got == want) {
+                                    if (++blk == g.nb) {  // the last block: leftover is the walks' to report
+                                        stop = true;
+                                        break;
+                                    }
+                                    if (++bx == g.per_row) {
+                                        bx = 0;
+                                        ++by;
+                                    }
+                                    want = g.sx(bx) * g.sy(by);
+                                    got = 0;
+                                }
+                            }
+                            if (stop) break;
+                            D = (int64_t)(ot - o0t);
+                            resume = q;
+                            publish();
+                            cand = ballot(test(e, ok, p0, o0, D, resume));
+                        }
+                    }
+                }
+                if (lane == 0) lds_st(&sh_done, (uint32_t)(j + 1));
+            }
+            if (lane == 0) lds_st(&sh_quit, 1u);
+            // chunks past a stop (an error or the stream's end inside a window: the walks before
+            // them report it) get a neutral entry; par_fix re-runs them if it ever reaches them
+            for (uint64_t c = next_chunk + lane; c < M.nchk; c += 64) {
+                C[c].q0 = hdr + c * span;
+                C[c].o_in = 0;
+                C[c].r_in = 0xFFu;
+            }
+            if (lane == 0) M.pfall = fall;
+        }
+        __syncthreads();
+    }
+}
+
+// one wave per chunk: the serial process from the predicted entry
+__global__ __launch_bounds__(256) void par_walk_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t items = ws.ctr[3];
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < items; t += (uint64_t)gridDim.x * 4) {
+        uint32_t i;
+        uint64_t j;
+        if (!sub_item(a, ws, t, i, j) || j % kSubPerChunk) continue;
+        const AMeta &M = ws.meta[i];
+        if (M.pfall) continue;
+        PChk &C = pchk(ws, M)[j / kSubPerChunk];
+        const uint64_t q = M.hdr + j * kSub;
+        const uint64_t qe = q + (uint64_t)kSub * kSubPerChunk < M.count ? q + (uint64_t)kSub * kSubPerChunk : M.count;
+        BWalk w;
+        w.init(M, at<uint8_t>(ws, M.sym), at<uint64_t>(ws, M.starts), lane);
+        const uint64_t q0 = C.q0;
+        if (q0 > q || q0 < M.hdr || C.r_in > 3) {  // no prediction: par_fix runs the chunk
+            if (lane == 0) C.r_q = 0xFFu;
+            continue;
+        }
+        w.enter(q0, C.r_in, C.o_in, q);
+        uint32_t r_q = C.r_in;
+        uint64_t o_q = C.o_in;
+        int st = 0;
+        if (q0 < q) {  // run in from the window's block start (recording nothing before q)
+            st = w.run(q, q);
+            r_q = st ? 0xFFu : w.r;
+            o_q = w.offset();
+        }
+        if (st == 0) st = w.run(qe, q);
+        if (lane == 0) {
+            C.r_q = r_q;
+            C.o_q = o_q;
+            C.st = (uint32_t)st;
+            C.r_out = w.r;
+            C.o_out = w.offset();
+        }
+    }
+}
+
+// one wave per stream: chunk entries against the exact exits before them, 64 chunks at a time
+// (lane k: chunk c, its predicted entry against chunk c - 1's exit); the first chunk that differs
+// (or every chunk, after a fallback) is re-run here from the exact exit, then the check goes on
+// after it; the first error in chunk order is the stream's status
+__global__ __launch_bounds__(64) void par_fix_kernel(DecArgs a, Ws ws)
+{
+    const uint32_t lane = lane_id();
+    for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+        AMeta &M = ws.meta[i];
+        if (M.status || !M.par) continue;
+        const PChk *C = pchk(ws, M);
+        BWalk w;
+        w.init(M, at<uint8_t>(ws, M.sym), at<uint64_t>(ws, M.starts), lane);
+        const Geo g = w.geo();
+        const bool fall = M.pfall != 0;
+        const uint64_t nchk = M.nchk, span = (uint64_t)kSub * kSubPerChunk;
+        uint32_t r = 0, st = 0;  // the exact process before chunk c
+        uint64_t o = 0, reruns = 0, c = 0;
+        while (c < nchk && !st) {
+            const uint64_t cl = c + lane;
+            const bool on = cl < nchk;
+            const uint32_t r_q = on ? C[cl].r_q : 0u, r_out = on ? C[cl].r_out : 0u, cst = on ? C[cl].st : 0u;
+            const uint64_t o_q = on ? C[cl].o_q : 0, o_out = on ? C[cl].o_out : 0;
+            // the exit before each lane's chunk: the lane below's (lane 0: the exact one)
+            const uint32_t pr = lane_shr1(r_out, r);
+            const uint64_t po = (uint64_t)lane_shr1((uint32_t)o_out, (uint32_t)o) |
+                                (uint64_t)lane_shr1((uint32_t)(o_out >> 32), (uint32_t)(o >> 32)) << 32;
+            // the walk matches the exact process if it entered at the same offset in the same
+            // state (at a block start the state is reset either way)
+            const bool same = !fall && r_q != 0xFFu && o_q == po && (r_q == pr || g.is_start(po));
+            const uint64_t bad = ballot(on && (!same || cst != 0));
+            if (!bad) {
+                const uint32_t last = (uint32_t)((nchk - c < 64 ? nchk - c : 64) - 1);
+                r = readlane(r_out, last);
+                o = (uint64_t)readlane((uint32_t)o_out, last) | (uint64_t)readlane((uint32_t)(o_out >> 32), last) << 32;
+                c += 64;
+                continue;
+            }
+            const uint32_t L = (uint32_t)__builtin_ctzll(bad);
+            c += L;  // chunks c .. c + L - 1 agree and end without an error
+            r = readlane(pr, L);
+            o = (uint64_t)readlane((uint32_t)po, L) | (uint64_t)readlane((uint32_t)(po >> 32), L) << 32;
+            if (readlane((uint32_t)same, L)) {  // an exact chunk that reports an error
+                st = readlane(cst, L);
+                break;
+            }
+            ++reruns;  // re-run chunk c from the exact process
+            const uint64_t q = M.hdr + c * span, qe = q + span < M.count ? q + span : M.count;
+            w.enter(q, r, o, q);
+            st = (uint32_t)w.run(qe, q);
+            r = w.r;
+            o = w.offset();
+            ++c;
+        }
+        if (lane == 0) {
+            M.status = (int32_t)st;
+            M.preruns = reruns;
+        }
     }
 }
 
@@ -2270,7 +3172,10 @@ uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t
 {
     // symbols <= 8 per payload byte (+64 slack); u64 block starts <= 8 (out_cap / 32 + 16) (see
     // group_entries_bound); chunk sums out_cap / 16384
-    return ws_header(n) + 8 * total_in + total_out / 4 + total_out / kChunk + 320ull * n + 4096;
+    // + the parallel boundary pass: <= 2.26 bytes per symbol of the streams that take it (Z
+    // entries and their window info 2, packed s0 0.25, records) and 4672 bytes of rounding per
+    // stream
+    return ws_header(n) + 27 * total_in + total_out / 4 + total_out / kChunk + 4992ull * n + 4096;
 }
 
 // Diagnostic stage clock (debug build only, hc_debug_stage_clock / hc_debug_stage_times): when
@@ -2369,6 +3274,21 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
     g_clock.mark("dec_header", st);
     bounds_kernel<<<resident_grid(bounds_kernel, 256), 256, 0, st>>>(a, ws);
     g_clock.mark("bounds", st);
+    // the parallel boundary pass for the streams of many block symbols (none: every launch
+    // finds no work item and returns)
+    const unsigned per_stream = b.n < kGrid ? b.n : kGrid;
+    par_fsm_kernel<<<resident_grid(par_fsm_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("par_fsm", st);
+    par_entry_kernel<<<per_stream, 64, 0, st>>>(a, ws);
+    g_clock.mark("par_entry", st);
+    par_z_kernel<<<resident_grid(par_z_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("par_z", st);
+    par_scan_kernel<<<per_stream, 64 * (kProd + 1), 0, st>>>(a, ws);
+    g_clock.mark("par_scan", st);
+    par_walk_kernel<<<resident_grid(par_walk_kernel, 256), 256, 0, st>>>(a, ws);
+    g_clock.mark("par_walk", st);
+    par_fix_kernel<<<per_stream, 64, 0, st>>>(a, ws);
+    g_clock.mark("par_fix", st);
     unblock_tile_kernel<<<resident_grid(unblock_tile_kernel, 256), 256, 0, st>>>(a, ws);
     g_clock.mark("unblock_tile", st);
     unblock_kernel<<<resident_grid(unblock_kernel, 256), 256, 0, st>>>(a, ws);
@@ -2387,6 +3307,12 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
 }  // namespace hc
 
 #ifdef HC_DEBUG_HOOKS
+extern "C" int hc_debug_set_par_min(uint64_t symbols)
+{
+    // block symbols from which an adaptive stream's boundaries take the parallel pass
+    return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_par_min), &symbols, sizeof(symbols)) == hipSuccess ? 0 : HC_ERR_DEVICE;
+}
+
 extern "C" int hc_debug_stage_clock(int on)
 {
     hc::g_clock.on = on != 0;

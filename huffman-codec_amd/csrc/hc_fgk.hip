@@ -23,6 +23,7 @@
 //    descriptors whose hardware range check replaces per-lane bounds tests.
 //  * Output bits gather in a 64-bit scalar accumulator, flush as big-endian dwords into a VGPR
 //    stage and leave as one coalesced 256-byte buffer store per 64 words.
+#include <mutex>
 #include <type_traits>
 
 #include "hc_internal.h"
@@ -980,9 +981,9 @@ struct RecSink {
 template <int kW, bool kTab = false>
 constexpr int kWavesPerSimd = kTab ? (kW == 0 ? 6 : 5) : (kW == 0 ? 8 : (kW == 1 ? 6 : 4));
 
-// Which way the encoder finds codes, voted per stream (status[] carries the vote, then the batch's
-// choice, until the encoder overwrites it with the stream's status): the path cache when the
-// stream's 16 most frequent
+// Which way the encoder finds codes, voted per stream (status[] carries the vote until the
+// encoder overwrites it with the stream's status; the two modes' launches run side by side on two
+// HIP streams, launch_encode_src): the path cache when the stream's 16 most frequent
 // symbols cover most of it (>= 60 %: the diff model's photos, 96 %), the level tables when the
 // alphabet is flat (< 15 %: noise, ramps, 6-8 %) -- measured: photo -c -m 8192 streams cache 67
 // ms / tables 131, noise -c -m 2048 485 / 227, ramps -c 8192 623 / 365 -- and in between (photos
@@ -1037,22 +1038,6 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
     }
     const bool cache = total == 0 || 100ull * top >= 60ull * total || (100ull * top >= 15ull * total && !low_occ);
     if (lane == 0) bt.status[sid] = cache ? kModeCache : kModeTables;
-}
-
-// The batch follows its majority: split between the cache and the table launches (which run one
-// after the other) each would hold only part of the GPU (measured: photo -c 8192 streams 600 ms
-// split by stream, against 402 / 427 ms in one mode)
-__global__ __launch_bounds__(1024) void enc_mode_vote_kernel(Batch bt)
-{
-    __shared__ uint32_t votes;
-    if (threadIdx.x == 0) votes = 0;
-    __syncthreads();
-    uint32_t v = 0;
-    for (uint32_t i = threadIdx.x; i < bt.n; i += 1024) v += bt.status[i] == kModeTables;
-    atomicAdd(&votes, v);
-    __syncthreads();
-    const int32_t mode = 2ull * votes > bt.n ? kModeTables : kModeCache;
-    for (uint32_t i = threadIdx.x; i < bt.n; i += 1024) bt.status[i] = mode;
 }
 
 template <int kW, int kSrc, bool kTab = false>
@@ -1818,16 +1803,48 @@ static uint32_t table_slots()
     return slots;
 }
 
-template <int kSrc>
-static void launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipStream_t st)
+// A second stream per device for the table-mode launches, so that they run beside the cache-mode
+// launches (never destroyed: the HIP runtime may be gone at exit; concurrent calls may share it,
+// each joins only its own work through its own events)
+static hipStream_t aux_stream()
 {
+    static std::mutex mu;
+    static hipStream_t aux[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!aux[dev] && hipStreamCreateWithFlags(&aux[dev], hipStreamNonBlocking) != hipSuccess) aux[dev] = nullptr;
+    return aux[dev];
+}
+
+template <int kSrc>
+static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipStream_t st)
+{
+    // every stream votes for its mode (enc_mode_kernel); the cache-mode launches run on the
+    // caller's stream and the table-mode launches beside them on the aux stream, each skipping
+    // the other mode's streams (so a mixed batch fills the GPU with both at once)
     enc_mode_kernel<kSrc><<<(b.n + 3) / 4, 256, 0, st>>>(b, b.n <= table_slots() ? 1u : 0u, enc_tab());
-    if (!enc_tab()) enc_mode_vote_kernel<<<1, 1024, 0, st>>>(b);
+    hipStream_t aux = aux_stream();
+    hipEvent_t fork = nullptr, join = nullptr;
+    if (aux && (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess))
+        aux = nullptr;
+    hipStream_t ts = st;  // the table-mode launches' stream
+    if (aux && hipEventRecord(fork, st) == hipSuccess && hipStreamWaitEvent(aux, fork, 0) == hipSuccess) ts = aux;
     encode_kernel<0, kSrc><<<grid, block, 0, st>>>(b);
-    encode_kernel<0, kSrc, true><<<grid, block, 0, st>>>(b);
+    encode_kernel<0, kSrc, true><<<grid, block, 0, ts>>>(b);
     encode_kernel<1, kSrc><<<grid, block, 0, st>>>(b);
-    encode_kernel<1, kSrc, true><<<grid, block, 0, st>>>(b);
+    encode_kernel<1, kSrc, true><<<grid, block, 0, ts>>>(b);
     encode_kernel<2, kSrc><<<grid, block, 0, st>>>(b);
+    hipError_t e = hipGetLastError();
+    if (ts != st) {
+        const hipError_t e1 = hipEventRecord(join, ts);
+        const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, join, 0) : e1;
+        if (e == hipSuccess) e = e2;
+    }
+    if (fork) (void)hipEventDestroy(fork);  // (released once the recorded work completes)
+    if (join) (void)hipEventDestroy(join);
+    return e;
 }
 
 hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st)
@@ -1839,11 +1856,10 @@ hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st)
     // enc_mode_kernel marks each stream for the cache or the table launch; then one launch per
     // tree layout and mode, each stream coded by exactly one of them (tree_kind, the mark)
     switch (src) {
-    case SRC_RAW: launch_encode_src<SRC_RAW>(b, grid, block, st); break;
-    case SRC_RAW_DIFF: launch_encode_src<SRC_RAW_DIFF>(b, grid, block, st); break;
-    default: launch_encode_src<SRC_SYMBOLS>(b, grid, block, st); break;
+    case SRC_RAW: return launch_encode_src<SRC_RAW>(b, grid, block, st);
+    case SRC_RAW_DIFF: return launch_encode_src<SRC_RAW_DIFF>(b, grid, block, st);
+    default: return launch_encode_src<SRC_SYMBOLS>(b, grid, block, st);
     }
-    return hipGetLastError();
 }
 
 hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)

@@ -371,6 +371,16 @@ def debug_set_enc_tab(mode):
         raise HCodecError(f"hc_debug_set_enc_tab failed: {rc}")
 
 
+def debug_set_par_min(symbols):
+    """Test hook (debug build only, use_debug_build): adaptive streams of at least `symbols` block
+    symbols find their block boundaries by the parallel pass (default 2^20; 0: every stream)."""
+    f = _dbg().hc_debug_set_par_min
+    f.argtypes = [ctypes.c_uint64]
+    rc = f(int(symbols))
+    if rc:
+        raise HCodecError(f"hc_debug_set_par_min failed: {rc}")
+
+
 def debug_stage_clock(on):
     """Diagnostic (debug build only, use_debug_build): when on, the batched adaptive calls of
     this thread record a HIP event after each stage; debug_stage_times() reads the last call's."""

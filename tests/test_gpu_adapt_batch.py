@@ -159,7 +159,8 @@ def test_stage_clock(gpu, hc, oracle_mod):
     assert st == [0] * 4 and dst == [0] * 4 and dec == raws
     assert [n for n, _ in enc_stages] == ["enc_plan", "tile_cost", "big_cost", "choose", "emit_tile", "emit_big",
                                          "fgk_encode", "status_fix"]
-    assert [n for n, _ in dec_stages] == ["dec_plan", "fgk_decode", "dec_header", "bounds", "unblock_tile",
+    assert [n for n, _ in dec_stages] == ["dec_plan", "fgk_decode", "dec_header", "bounds", "par_fsm", "par_entry",
+                                         "par_z", "par_scan", "par_walk", "par_fix", "unblock_tile",
                                          "unblock", "chunk_sum", "chunk_scan", "undiff", "dec_final"]
     assert all(ms >= 0 for _, ms in enc_stages + dec_stages)
     try:
