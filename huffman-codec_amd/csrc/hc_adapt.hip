@@ -2312,29 +2312,35 @@ __device__ __forceinline__ uint32_t s0_at(const uint32_t *pk, uint64_t rel)
 
 // One workgroup per stream: Z in order with the running correction D
 // (tests/bounds_par_model.py). The serial part -- D changes at every block start found in Z --
-// is one wave (the consumer); the other 15 (producers) run up to kRing sub-chunks ahead of it:
-// each loads a sub-chunk's record, Z entries and window infos into an LDS ring slot and tests
-// them against the D the consumer last published (a version of it), noting the first candidate
-// and loading the symbols around it. The consumer takes a slot whose test used the current
-// version as it is (no candidate: nothing to do), and tests it again otherwise (after a block
-// start found since). A block start in Z whose window par_z could describe (not split by a block
-// end or a chunk start) takes D += its correction at once; any other is simulated symbol by
-// symbol, from the slot's prefetched window when it is that one.
+// is one wave (the consumer); the other kProd (producers) run up to kRing sub-chunks ahead of it:
+// each loads a sub-chunk's record and Z entries with their window infos into an LDS ring slot
+// (a dense sub-chunk: every symbol as an entry, with its symbols and states), notes in a bitmap
+// the residues mod B^2 of the entries' no-reset offsets (hashed to 1024 bits), and tests the
+// entries against the D the consumer last published (a version of it), noting the first
+// candidate and loading the symbols around it. The consumer takes a slot whose test used the
+// current version as it is; after a block start found since, the bitmap tells in one read whether
+// any entry can be one under the new D (else the slot's entries are tested again). A block start
+// in Z whose window par_z could describe (not split by a block end or a chunk start) takes D +=
+// its correction at once; any other is simulated symbol by symbol, its window from the slot.
 constexpr uint32_t kZr = kZcap / 64;  // Z entries per lane and sub-chunk
-constexpr uint32_t kRing = 12;        // ring slots (sub-chunks ahead of the consumer)
+constexpr uint32_t kRing = 10;        // ring slots (sub-chunks ahead of the consumer)
 constexpr uint32_t kSpinCap = 1u << 23;  // sleeps before a wait gives up (~1 s; never expected)
 constexpr uint32_t kProd = 11;        // producer waves (12 waves per workgroup: registers for the consumer's paths)
 struct RSlot {
     uint32_t j;      // the sub-chunk published here (0xFFFFFFFF: none yet)
     uint32_t ver;    // the D version its test used
     uint32_t first;  // first candidate under that version: entry index (dense: symbol index), ~0 none
-    uint32_t zn;     // entries (kDense: dense, no entries here)
+    uint32_t zn;     // entries (kDense: dense, every symbol an entry)
     uint32_t s0, L;
     uint64_t o0;
     uint64_t wz;     // the prefetched window's block start (~0: none)
     uint32_t wx[16];  // symbols wz - 1 .. wz + 62
     uint32_t ws[4];   // s0 of wz .. wz + 63: bit planes (low 64 bits, high 64 bits)
-    uint32_t ze[kZcap], zi[kZcap];
+    uint32_t bm[32];  // residues (o0 + rel) mod B^2 (mod 1024) of the entries present
+    uint32_t ze[kSub];          // entries: Z (zn of them) or, dense, all symbols (offset << 11 | index)
+    uint32_t zi[kZcap];         // window infos (Z entries)
+    uint32_t sx[kSub / 4];      // dense: the symbols (p0 .. p0 + cnt)
+    uint32_t sp[kSub / 16];     // dense: packed s0
 };
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2342,7 +2348,6 @@ __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { __atomic_store
 __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, Ws ws)
 {
     __shared__ RSlot ring[kRing];
-    __shared__ uint32_t OD[kSub];            // consumer: a dense sub-chunk's no-reset offsets
     __shared__ int64_t vD[64];                // D of version v at [v % 64]
     __shared__ uint64_t vres[64];             // resume of version v
     __shared__ uint32_t sh_ver, sh_done, sh_quit;
@@ -2408,29 +2413,6 @@ __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, W
             else hit = ok && g.is_start(base + rel);
             return ok && pr >= rres && hit;
         };
-        // dense sub-chunk j: each of this lane's 32 symbols (32 lane + q) with its no-reset offset in
-        // the sub-chunk, handed to f(q, offset) in order (two passes over the loaded symbols: no
-        // per-symbol arrays)
-        auto dense_each = [&](uint64_t j, uint64_t p0, uint32_t cnt, auto f) __attribute__((always_inline)) {
-            uint32_t w[8];
-            (void)load_sub(sym, hdr, p0, p0 + cnt, lane, w);
-            const uint32_t s0lo = pk[j * (kSub / 16) + 2 * lane], s0hi = pk[j * (kSub / 16) + 2 * lane + 1];
-            auto len = [&](uint32_t q) __attribute__((always_inline)) {
-                const uint32_t x = (w[q >> 2] >> (8 * (q & 3))) & 255u;
-                const uint32_t s0 = ((q < 16 ? s0lo : s0hi) >> (2 * (q & 15))) & 3u;
-                return 32 * lane + q < cnt ? (s0 == 3 ? x : 1u) : 0u;
-            };
-            uint32_t tot = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 32; ++q) tot += len(q);
-            const uint32_t inc = wave_sum_incl(tot);
-            uint32_t acc = inc - tot;
-#pragma unroll
-            for (uint32_t q = 0; q < 32; ++q) {
-                f(q, acc);
-                acc += len(q);
-            }
-        };
         if (wv > 0) {
             // ------------------------------------------------------------- producers
             for (uint64_t j = wv - 1; j < nsub; j += kProd) {
@@ -2449,49 +2431,73 @@ __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, W
                 const uint64_t p0 = hdr + j * kSub;
                 const uint32_t cnt = (uint32_t)((p0 + kSub < n ? p0 + kSub : n) - p0);
                 const bool dense = rec.zn == kDense;
-                uint32_t e[kZr], zi[kZr];
+                const uint32_t items = dense ? cnt : rec.zn;
+                if (lane < 32) R.bm[lane] = pow2 ? 0u : 0xFFFFFFFFu;
+                __builtin_amdgcn_wave_barrier();
                 if (!dense) {
+                    uint32_t e[kZr], zi[kZr];
 #pragma unroll
                     for (uint32_t r = 0; r < kZr; ++r) {
                         const uint32_t it = 64 * r + lane;
-                        e[r] = it < rec.zn ? Zall[j * kZcap + it] : 0xFFFFFFFFu;
-                        zi[r] = it < rec.zn ? ZIall[j * kZcap + it] : 0u;
-                    }
-                }
-                // the consumer's current version of (D, resume)
-                const uint32_t v = lds_ld(&sh_ver);
-                const int64_t D = vD[v % 64];
-                const uint64_t resume = vres[v % 64];
-                uint32_t first = 0xFFFFFFFFu;
-                if (!dense) {
-#pragma unroll
-                    for (int r = kZr - 1; r >= 0; --r) {
-                        const uint64_t m = ballot(test(e[r], e[r] != 0xFFFFFFFFu, p0, rec.o0, D, resume));
-                        if (m) first = 64 * r + (uint32_t)__builtin_ctzll(m);
+                        e[r] = it < items ? Zall[j * kZcap + it] : 0xFFFFFFFFu;
+                        zi[r] = it < items ? ZIall[j * kZcap + it] : 0u;
                     }
 #pragma unroll
                     for (uint32_t r = 0; r < kZr; ++r) {
                         R.ze[64 * r + lane] = e[r];
                         R.zi[64 * r + lane] = zi[r];
+                        if (pow2 && e[r] != 0xFFFFFFFFu) {
+                            const uint32_t res = (uint32_t)((rec.o0 + (e[r] >> 11)) & mask) & 1023u;
+                            __hip_atomic_fetch_or(&R.bm[res >> 5], 1u << (res & 31), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        }
                     }
-                } else {
-                    uint64_t any = 0;
-                    uint32_t fq = 0xFFFFFFFFu;
-                    dense_each(j, p0, cnt, [&](uint32_t q, uint32_t od) __attribute__((always_inline)) {
-                        const bool h = test((od << 11) | (32 * lane + q), 32 * lane + q < cnt, p0, rec.o0, D, resume);
-                        fq = h && fq == 0xFFFFFFFFu ? 32 * lane + q : fq;
-                    });
-                    any = ballot(fq != 0xFFFFFFFFu);
-                    if (any) first = readlane(fq, (uint32_t)__builtin_ctzll(any));  // lanes hold ascending symbols
-                }
-                // the window around the first candidate: symbols z - 1 .. z + 62, s0 of z .. z + 63
-                uint64_t wz = ~0ull;
-                if (first != 0xFFFFFFFFu) {
-                    const uint32_t ef = dense ? first : (readlane(e[0], first & 63) & 2047u);
-                    uint32_t efr = e[0];
+                } else {  // every symbol: its no-reset offset from s0 and lengths
+                    uint32_t w[8];
+                    (void)load_sub(sym, hdr, p0, p0 + cnt, lane, w);
+                    const uint32_t s0lo = pk[j * (kSub / 16) + 2 * lane], s0hi = pk[j * (kSub / 16) + 2 * lane + 1];
+                    auto len = [&](uint32_t q) __attribute__((always_inline)) {
+                        const uint32_t x = (w[q >> 2] >> (8 * (q & 3))) & 255u;
+                        const uint32_t s0 = ((q < 16 ? s0lo : s0hi) >> (2 * (q & 15))) & 3u;
+                        return 32 * lane + q < cnt ? (s0 == 3 ? x : 1u) : 0u;
+                    };
+                    uint32_t tot = 0;
 #pragma unroll
-                    for (uint32_t r = 1; r < kZr; ++r) efr = (first >> 6) == r ? e[r] : efr;
-                    wz = p0 + (dense ? ef : (readlane(efr, first & 63) & 2047u));
+                    for (uint32_t q = 0; q < 32; ++q) tot += len(q);
+                    const uint32_t inc = wave_sum_incl(tot);
+                    uint32_t acc = inc - tot;
+#pragma unroll
+                    for (uint32_t q = 0; q < 32; ++q) {
+                        const uint32_t idx = 32 * lane + q;
+                        R.ze[idx] = idx < cnt ? (acc << 11) | idx : 0xFFFFFFFFu;
+                        if (pow2 && idx < cnt) {
+                            const uint32_t res = (uint32_t)((rec.o0 + acc) & mask) & 1023u;
+                            __hip_atomic_fetch_or(&R.bm[res >> 5], 1u << (res & 31), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        }
+                        acc += len(q);
+                    }
+#pragma unroll
+                    for (uint32_t k = 0; k < 8; ++k) R.sx[8 * lane + k] = w[k];
+                    R.sp[2 * lane] = s0lo;
+                    R.sp[2 * lane + 1] = s0hi;
+                }
+                __builtin_amdgcn_wave_barrier();
+                // the consumer's current version of (D, resume), and the first candidate under it
+                const uint32_t v = lds_ld(&sh_ver);
+                const int64_t D = vD[v % 64];
+                const uint64_t resume = vres[v % 64];
+                uint32_t first = 0xFFFFFFFFu;
+                for (uint32_t b = 0; b < items && first == 0xFFFFFFFFu; b += 64) {
+                    const uint32_t e = b + lane < items ? R.ze[b + lane] : 0xFFFFFFFFu;
+                    const uint64_t m = ballot(test(e, e != 0xFFFFFFFFu, p0, rec.o0, D, resume));
+                    if (m) first = b + (uint32_t)__builtin_ctzll(m);
+                }
+                // the window around it (a Z entry's; a dense sub-chunk has its symbols in the slot):
+                // symbols z - 1 .. z + 62, s0 of z .. z + 63
+                uint64_t wz = ~0ull;
+                if (first != 0xFFFFFFFFu && !dense) {
+                    wz = p0 + (R.ze[first] & 2047u);
                     const uint64_t pl = wz + lane;
                     const uint32_t x = pl - 1 < n ? sym[pl - 1] : 0u;
                     const uint32_t s0q = pl < n ? s0_at(pk, pl - hdr) : 0u;
@@ -2525,6 +2531,18 @@ __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, W
             uint64_t next_chunk = 0;
             bool stop = false;     // an error or the end inside a window: the walks report it
             uint32_t fall = 0;
+#ifdef HC_DEBUG_HOOKS
+            // cycles: slot waits, tests, slow hits; counts: subs tested again, skipped by the
+            // bitmap, fast hits, slow hits, dense subs
+            uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PDG_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PDG_ADD(k, t0) (dg[k] += __builtin_amdgcn_s_memtime() - (t0))
+#define PDG_CNT(k) (++dg[k])
+#else
+#define PDG_T(v)
+#define PDG_ADD(k, t0)
+#define PDG_CNT(k)
+#endif
             auto publish = [&]() __attribute__((always_inline)) {
                 ++ver;
                 if (lane == 0) {
@@ -2537,6 +2555,7 @@ __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, W
             };
             for (uint64_t j = 0; j < nsub && !stop; ++j) {
                 RSlot &R = ring[j % kRing];
+                PDG_T(t_w);
                 for (uint32_t spin = 0; lds_ld(&R.j) != (uint32_t)j; ++spin) {
                     if (lds_ld(&sh_quit) || spin > kSpinCap) {  // (a producer gave up: never expected)
                         fall = 1;
@@ -2545,6 +2564,7 @@ __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, W
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+                PDG_ADD(0, t_w);
                 if (stop) break;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 const uint64_t p0 = hdr + j * kSub;
@@ -2562,116 +2582,167 @@ __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, W
                 const bool dense = zn == kDense;
                 const uint32_t cnt = (uint32_t)((p0 + kSub < n ? p0 + kSub : n) - p0);
                 const uint32_t items = dense ? cnt : zn;
-                // the producer's test holds while no block start was found since it ran
-                if (!(rv == ver && rfirst == 0xFFFFFFFFu)) {
-                    if (dense) {
-                        dense_each(j, p0, cnt, [&](uint32_t q, uint32_t od) __attribute__((always_inline)) {
-                            OD[32 * lane + q] = od;
-                        });
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                    const uint32_t b_first = rv == ver ? (rfirst & ~63u) : 0u;
-                    for (uint32_t b = b_first; b < items && !stop; b += 64) {
-                        const bool ok = b + lane < items;
-                        const uint32_t e = ok ? (dense ? (OD[b + lane] << 11) | (b + lane) : R.ze[b + lane]) : 0xFFFFFFFFu;
-                        uint64_t cand = ballot(test(e, ok, p0, o0, D, resume));
-                        while (cand && !stop) {
-                            const uint32_t L = (uint32_t)__builtin_ctzll(cand);
-                            const uint32_t eL = readlane(e, L);
-                            const uint32_t ziL = dense ? 0u : R.zi[b + L];
-                            const uint64_t z = p0 + (eL & 2047u);
-                            const uint64_t oz0 = o0 + (eL >> 11);  // O0(z)
-                            const uint64_t o = oz0 + D;
-                            // fast path: the window par_z described, inside one block (B^2 bytes),
-                            // no chunk start inside it
-                            const uint32_t wl = ziL & 63u, wo = ziL >> 19;
-                            const uint64_t cz = (z - hdr) / span, cw = (z + wl - 1 - hdr) / span;
-                            if (ziL && o < full_end && mask + 1 > wo && cz == cw) {
-                                D += (int64_t)((ziL >> 6) & 8191u) - 4096;
-                                resume = z + wl;
-                                publish();
-                                cand = ballot(test(e, ok, p0, o0, D, resume));
-                                continue;
+                // the producer's test holds while no block start was found since it ran; after
+                // one, the bitmap says whether any entry has the residue a start needs now (when
+                // every entry is in the full block rows)
+                bool skip = rv == ver && rfirst == 0xFFFFFFFFu;
+                if (!skip && rv != ver && pow2 && o0 + D + R.L < full_end) {
+                    // a start needs (o0 + rel + D) = 0 mod B^2: residue (o0 + rel) = -D
+                    const uint32_t want = (uint32_t)((0 - (uint64_t)D) & mask) & 1023u;
+                    skip = ((R.bm[want >> 5] >> (want & 31)) & 1u) == 0;
+                    if (skip) PDG_CNT(4);
+                }
+                PDG_T(t_t);
+                if (!skip) {
+                    PDG_CNT(3);
+                    if (dense) PDG_CNT(7);
+                    // the batches of 64 entries that can hold a start under (D, resume), lane k
+                    // for batch k: entries are sorted by offset, so batch k's offsets span
+                    // [first, last] and a start needs one = -(o0 + D) mod B^2 in that range
+                    auto batches = [&]() __attribute__((always_inline)) -> uint64_t {
+                        const uint32_t nbt = (items + 63) / 64, k = lane;
+                        bool maybe = false;
+                        if (k < nbt) {
+                            const uint32_t ef = R.ze[64 * k], el = R.ze[min(64 * k + 63, items - 1)];
+                            const uint32_t rf = ef >> 11, rl = el >> 11;
+                            const uint64_t base = o0 + D;
+                            maybe = true;
+                            if (pow2 && base + rl < full_end) {
+                                const uint32_t t = (uint32_t)((0 - base) & mask);
+                                maybe = ((t - rf) & (uint32_t)mask) <= rl - rf;
                             }
-                            // the true machine from the block start z until it rejoins s0; the
-                            // window from the slot when the producer prefetched this one
-                            uint64_t ot = o, o0t = oz0, got = 0, want;
+                            const uint32_t rres = resume <= p0 ? 0u : (resume - p0 >= kSub ? kSub : (uint32_t)(resume - p0));
+                            if ((el & 2047u) < rres) maybe = false;  // the whole batch is behind resume
+                        }
+                        return ballot(maybe);
+                    };
+                    uint64_t bmask = batches();
+                    if (rv == ver && rfirst != 0xFFFFFFFFu) bmask &= ~0ull << (rfirst >> 6);
+                    while (bmask && !stop) {
+                        const uint32_t bk = (uint32_t)__builtin_ctzll(bmask), b = 64 * bk;
+                        const bool ok = b + lane < items;
+                        const uint32_t e = ok ? R.ze[b + lane] : 0xFFFFFFFFu;
+                        const uint64_t cand = ballot(test(e, ok, p0, o0, D, resume));
+                        if (!cand) {
+                            bmask &= bmask - 1;
+                            continue;
+                        }
+                        const uint32_t idx = b + (uint32_t)__builtin_ctzll(cand);
+                        const uint32_t eL = R.ze[idx];
+                        const uint32_t ziL = dense ? 0u : R.zi[idx];
+                        const uint64_t z = p0 + (eL & 2047u);
+                        const uint64_t oz0 = o0 + (eL >> 11);  // O0(z)
+                        const uint64_t o = oz0 + D;
+                        // fast path: the window par_z described, inside one block (B^2 bytes),
+                        // no chunk start inside it
+                        const uint32_t wl = ziL & 63u, wo = ziL >> 19;
+                        const uint64_t cz = (z - hdr) / span, cw = (z + wl - 1 - hdr) / span;
+                        if (ziL && o < full_end && mask + 1 > wo && cz == cw) {
+                            PDG_CNT(5);
+                            D += (int64_t)((ziL >> 6) & 8191u) - 4096;
+                            resume = z + wl;
+                            publish();
+                            bmask = batches() & (~0ull << bk);
+                            continue;
+                        }
+                        PDG_CNT(6);
+                        PDG_T(t_h);
+                        // the true machine from the block start z until it rejoins s0; the
+                        // window from the slot (a dense sub-chunk's symbols, or the one the
+                        // producer prefetched) while it lasts. Blocks in the full rows hold
+                        // B^2 bytes; elsewhere the block's place gives its size.
+                        uint64_t ot = o, o0t = oz0, got = 0, want;
+                        if (o < full_end) {
+                            want = mask + 1;
+                        } else {
                             uint64_t bx, by, rl;
                             g.locate(ot, bx, by, rl);
                             want = g.sx(bx) * g.sy(by);
-                            uint64_t blk = by * g.per_row + bx;
-                            uint32_t u = 0;
-                            uint64_t q = z;
-                            uint32_t xw = 0, sw0 = 0;  // window: symbols q - 1 + lane, s0 of q + lane
-                            uint64_t wbase = ~0ull;
-                            if (R.wz == z) {
-                                wbase = z;
-                                xw = reinterpret_cast<const uint8_t *>(R.wx)[lane];
-                                const uint64_t p0l = (uint64_t)R.ws[1] << 32 | R.ws[0], p1l = (uint64_t)R.ws[3] << 32 | R.ws[2];
-                                sw0 = (uint32_t)((p0l >> lane) & 1u) | (uint32_t)(((p1l >> lane) & 1u) << 1);
-                            }
-                            for (;;) {
-                                if (q > z && got == 0) u = 0;  // a block start inside the window
-                                if (q >= n) {
-                                    stop = true;
-                                    break;
-                                }
-                                if (q - z >= kWinCap) {
-                                    fall = 1;
-                                    stop = true;
-                                    break;
-                                }
-                                if (wbase == ~0ull || q - wbase >= 63) {  // (re)load the window at q
-                                    wbase = q;
-                                    const uint64_t pl = q + lane;
-                                    xw = pl - 1 < n ? sym[pl - 1] : 0u;
-                                    sw0 = pl < n ? s0_at(pk, pl - hdr) : 0u;
-                                }
-                                const uint32_t s0q = readlane(sw0, (uint32_t)(q - wbase));
-                                if (q > z && u == s0q) break;  // rejoined
-                                if ((q - hdr) % span == 0 && q > z) {
-                                    // a chunk start inside the window: its walk runs in from z
-                                    const uint64_t c = (q - hdr) / span;
-                                    if (lane == 0) {
-                                        C[c].q0 = z;
-                                        C[c].o_in = oz0 + D;
-                                        C[c].r_in = 0;
-                                    }
-                                    next_chunk = c + 1;
-                                }
-                                const uint32_t x = readlane(xw, (uint32_t)(q - wbase) + 1);
-                                const uint32_t xp = readlane(xw, (uint32_t)(q - wbase));
-                                const uint32_t lt = u == 3 ? x : 1u;
-                                o0t += s0q == 3 ? x : 1u;
-                                ot += lt;
-                                got += lt;
-                                u = fsm_at(fsm_step(x, xp), u);
-                                ++q;
-                                if (got > want) {  // overshoot: status 13, reported by the walks
-                                    stop = true;
-                                    break;
-                                }
-                                if (got == want) {
-                                    if (++blk == g.nb) {  // the last block: leftover is the walks' to report
-                                        stop = true;
-                                        break;
-                                    }
-                                    if (++bx == g.per_row) {
-                                        bx = 0;
-                                        ++by;
-                                    }
-                                    want = g.sx(bx) * g.sy(by);
-                                    got = 0;
-                                }
-                            }
-                            if (stop) break;
-                            D = (int64_t)(ot - o0t);
-                            resume = q;
-                            publish();
-                            cand = ballot(test(e, ok, p0, o0, D, resume));
                         }
+                        uint32_t u = 0;
+                        uint64_t q = z;
+                        uint32_t xw = 0, sw0 = 0;  // window: symbols q - 1 + lane, s0 of q + lane
+                        uint64_t wbase = ~0ull;
+                        auto load_window = [&]() __attribute__((always_inline)) {
+                            wbase = q;
+                            const uint64_t pl = q + lane;
+                            const uint64_t r1 = pl - 1 - p0, r0 = pl - p0;
+                            if (dense && pl - 1 >= p0 && r1 < cnt) {
+                                xw = reinterpret_cast<const uint8_t *>(R.sx)[r1];
+                            } else {
+                                xw = pl - 1 < n ? sym[pl - 1] : 0u;
+                            }
+                            if (dense && r0 < cnt) {
+                                sw0 = (R.sp[r0 >> 4] >> (2 * (r0 & 15))) & 3u;
+                            } else {
+                                sw0 = pl < n ? s0_at(pk, pl - hdr) : 0u;
+                            }
+                        };
+                        if (!dense && R.wz == z) {
+                            wbase = z;
+                            xw = reinterpret_cast<const uint8_t *>(R.wx)[lane];
+                            const uint64_t p0l = (uint64_t)R.ws[1] << 32 | R.ws[0], p1l = (uint64_t)R.ws[3] << 32 | R.ws[2];
+                            sw0 = (uint32_t)((p0l >> lane) & 1u) | (uint32_t)(((p1l >> lane) & 1u) << 1);
+                        }
+                        for (;;) {
+                            if (q > z && got == 0) u = 0;  // a block start inside the window
+                            if (q >= n) {
+                                stop = true;
+                                break;
+                            }
+                            if (q - z >= kWinCap) {
+                                fall = 1;
+                                stop = true;
+                                break;
+                            }
+                            if (wbase == ~0ull || q - wbase >= 63) load_window();  // (re)load at q
+                            const uint32_t s0q = readlane(sw0, (uint32_t)(q - wbase));
+                            if (q > z && u == s0q) break;  // rejoined
+                            if ((q - hdr) % span == 0 && q > z) {
+                                // a chunk start inside the window: its walk runs in from z
+                                const uint64_t c = (q - hdr) / span;
+                                if (lane == 0) {
+                                    C[c].q0 = z;
+                                    C[c].o_in = oz0 + D;
+                                    C[c].r_in = 0;
+                                }
+                                next_chunk = c + 1;
+                            }
+                            const uint32_t x = readlane(xw, (uint32_t)(q - wbase) + 1);
+                            const uint32_t xp = readlane(xw, (uint32_t)(q - wbase));
+                            const uint32_t lt = u == 3 ? x : 1u;
+                            o0t += s0q == 3 ? x : 1u;
+                            ot += lt;
+                            got += lt;
+                            u = fsm_at(fsm_step(x, xp), u);
+                            ++q;
+                            if (got > want) {  // overshoot: status 13, reported by the walks
+                                stop = true;
+                                break;
+                            }
+                            if (got == want) {  // the next block starts at offset ot
+                                got = 0;
+                                if (ot < full_end) {
+                                    want = mask + 1;
+                                } else if (ot >= g.total) {  // the last block: leftover is the walks' to report
+                                    stop = true;
+                                    break;
+                                } else {  // the last block row or another geometry
+                                    uint64_t bx, by, rl;
+                                    g.locate(ot, bx, by, rl);
+                                    want = g.sx(bx) * g.sy(by);
+                                }
+                            }
+                        }
+                        PDG_ADD(2, t_h);
+                        if (stop) break;
+                        D = (int64_t)(ot - o0t);
+                        resume = q;
+                        publish();
+                        bmask = batches() & (~0ull << bk);
                     }
                 }
+                PDG_ADD(1, t_t);
                 if (lane == 0) lds_st(&sh_done, (uint32_t)(j + 1));
             }
             if (lane == 0) lds_st(&sh_quit, 1u);
@@ -2683,6 +2754,14 @@ __global__ __launch_bounds__(64 * (kProd + 1)) void par_scan_kernel(DecArgs a, W
                 C[c].r_in = 0xFFu;
             }
             if (lane == 0) M.pfall = fall;
+#ifdef HC_DEBUG_HOOKS
+            if (lane < 8) {
+                uint64_t dv = dg[0];
+#pragma unroll
+                for (uint32_t k = 1; k < 8; ++k) dv = lane == k ? dg[k] : dv;
+                M.pdiag[lane] = dv;
+            }
+#endif
         }
         __syncthreads();
     }

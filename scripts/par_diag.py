@@ -34,3 +34,7 @@ for use_diff in (False, True):
     m32 = meta.view("uint32")
     print(f"{'-c -a -m' if use_diff else '-c -a'}: parallel pass {m32[356 // 4]}, fallback {m32[360 // 4]},"
           f" sub-chunks {m64[408 // 8]}, chunks {m64[416 // 8]}, chunks re-run by par_fix {m64[424 // 8]}")
+    d = m64[432 // 8:496 // 8]
+    us = lambda c: f"{c / 2400:.0f} us"  # s_memtime: the shader clock, ~2.4 GHz
+    print(f"  par_scan consumer: slot waits {us(d[0])}, tests {us(d[1])} (slow hits {us(d[2])}); sub-chunks"
+          f" tested again {d[3]} (dense {d[7]}), skipped by the bitmap {d[4]}, fast hits {d[5]}, slow hits {d[6]}")
