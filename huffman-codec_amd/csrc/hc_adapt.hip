@@ -47,13 +47,6 @@ namespace {
 // (load, equality words, candidates, summaries) into g_tc_prof (hc_debug_tc_prof reads it).
 #ifdef HC_TC_PROF
 __device__ unsigned long long g_tc_prof[4];
-#define HC_TC_BEGIN() uint64_t tc_t = __builtin_amdgcn_s_memtime()
-#define HC_TC_MARK(i)                                                                              \
-    do {                                                                                           \
-        const uint64_t tc_n = __builtin_amdgcn_s_memtime();                                        \
-        if (tid == 0) atomicAdd(&g_tc_prof[(i) - 1], (unsigned long long)(tc_n - tc_t));           \
-        tc_t = tc_n;                                                                               \
-    } while (0)
 #else
 #define HC_TC_BEGIN()
 #define HC_TC_MARK(i)
@@ -640,48 +633,6 @@ __device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileA
     lds_barrier();
 }
 
-// The same image in one go with few registers (emit_tile_kernel, whose occupancy the prefetch
-// registers would halve): 4 items per thread in flight; with dword-aligned rows the diff
-// model's previous byte is the top byte of the dword before, which the lane below loaded
-// (wave_shr 1; lane 0 loads it again).
-__device__ __forceinline__ void load_tile(uint8_t *D, const uint8_t *mat, uint64_t n, uint64_t W, uint64_t tx0,
-                                          uint64_t ty0, uint32_t tw, uint32_t th, bool diff, uint32_t tid)
-{
-    const uint32_t nd = (tw + 7) / 4, items = (th + 1) * nd;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(mat) | W) & 3) == 0;
-    const uint32_t lane = tid & 63;
-    constexpr int kU = 4;
-    for (uint32_t base = 0; base < items; base += 256 * kU) {
-        uint32_t v[kU], pv[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint32_t it = base + u * 256 + tid;
-            const uint32_t r = it / nd, d = it - r * nd;
-            const int64_t lin = (int64_t)(ty0 + r) * (int64_t)W - (int64_t)W + (int64_t)tx0 - 4 + 4 * (int64_t)d;
-            const bool on = it < items && (r > 0 || ty0 > 0);
-            if (aligned) {
-                const bool whole = on && lin >= 0 && (uint64_t)lin + 4 <= n;
-                v[u] = whole ? *reinterpret_cast<const uint32_t *>(mat + lin) : (on ? load4(mat, lin, n) : 0u);
-                const uint32_t below = lane_shr1(v[u], 0u);
-                const bool own = on && diff && lane == 0 && d > 0;
-                pv[u] = own ? load4(mat, lin - 4, n) : below;  // the dword before (d > 0)
-                pv[u] = (pv[u] >> 24) | (v[u] << 8);         // bytes lin - 1 .. lin + 2
-            } else {
-                v[u] = on ? load4(mat, lin, n) : 0u;
-                pv[u] = on && diff ? load4(mat, lin - 1, n) : 0u;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint32_t it = base + u * 256 + tid;
-            if (it < items) {
-                const uint32_t r = it / nd, d = it - r * nd;
-                *reinterpret_cast<uint32_t *>(D + r * kDS + 4 * d) = diff ? sub8(v[u], pv[u]) : v[u];
-            }
-        }
-    }
-}
-
 // the value of lane l + d (d a power of two): DPP row_shl inside 16-lane rows, else a permute
 __device__ __forceinline__ uint32_t shl_down(uint32_t v, uint32_t d)
 {
@@ -860,7 +811,10 @@ __device__ __forceinline__ void stats128(const uint64_t *E, const uint64_t *WM, 
 // wrap masks of a whole tile), 3. every candidate's block costs (fast_cost / stats128 on whole
 // tiles, the run-segment monoid on partial ones) into the cost words and per-candidate totals,
 // 4. the tile row / column summaries the blocks of B >= 256 are joined from (big_cost_kernel).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_cost_kernel(EncArgs a, Ws ws)
+#ifndef HC_TC_WPE
+#define HC_TC_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))) void tile_cost_kernel(EncArgs a, Ws ws)
 {
     __shared__ uint8_t D[(kTile + 1) * kDS];  // DT(r, xl): y = ty0 + r - 1, x = tx0 + xl
     __shared__ uint64_t E[4 * kTile];         // Eh[r][2] then Ev[c][2]
@@ -1323,48 +1277,85 @@ __device__ __forceinline__ uint32_t count_below(uint64_t m)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// per lane: bit lane of m ? t : f (one v_cndmask on a scalar mask: no exec-mask branch)
+__device__ __forceinline__ uint32_t sel(uint64_t m, uint32_t t, uint32_t f)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+// leading zeros of x, 0xFFFFFFFF for 0 (v_ffbh_u32 without the zero test)
+__device__ __forceinline__ uint32_t ffbh(uint32_t x)
+{
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kDrop = 0x7FFFFFF8u;  // buffer offset past every range: the store is dropped
+__device__ __forceinline__ rsrc_t out_rsrc(uint8_t *p)
+{
+    // (readfirstlane: a pointer the compiler cannot prove uniform would get a waterfall loop)
+    const uint64_t a = (uint64_t)p;
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32;
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint8_t *>(u), (short)0, 0x7FFFFFF0, 0x00020000);
+}
+
 // emit_block for whole blocks of a tile image (L = B * B, a multiple of 64): no lane is past
 // the block, so only the last step has the last-element rules; element p = 64 s + lane sits at
 // LDS byte a(s) = a(0) + (s >> 1) dA + (s & 1) dB (B <= 64: dA = 2 dB, one step = 64 / B whole
-// lines; B = 128: half a line), so each step's read costs one add; positions from v_mbcnt; the
-// previous value 0x100 before element 0 (no byte equals it) starts its run.
+// lines; B = 128: half a line), so each step's read costs one add; the previous value 0x100
+// before element 0 (no byte equals it) starts its run. Branch-free: the emit rules are lane masks
+// (ballots), a lane's bytes go out through a buffer store whose offset is out of range when it
+// emits none. Per element with j = run offset mod 258 (transform.cpp:241-279): it emits when
+// it is the block's last (a literal), j <= 2 (a literal), j = 257 (count 255) or its run ends
+// (count j - 2); j = 2 at a run's end emits the literal and the count 0.
 struct EmitWhole {
-    uint32_t addr, dA, dB, pv, po, v;
-    uint64_t q;
-    uint8_t *out;
+    uint32_t addr, dA, dB, pv, po, v, vn, q;
+    rsrc_t rs;
     __device__ __forceinline__ void init(const uint8_t *D, uint32_t a0, uint32_t dA_, uint32_t dB_, uint8_t *o)
     {
-        addr = a0;
+        addr = a0 + dB_;
         dA = dA_;
         dB = dB_;
         pv = 0x100;  // differs from every byte: element 0 starts a run
         po = 0;
         q = 0;
-        out = o;
-        v = D[addr];
+        rs = out_rsrc(o);
+        v = D[a0];
+        vn = D[addr];
     }
-    // step s (elements 64 s .. 64 s + 63); fin: the block's last step
-    __device__ __forceinline__ void step(const uint8_t *D, uint32_t s, bool fin, uint32_t lane, uint64_t lte)
+    // step s (elements 64 s .. 64 s + 63); fin: the block's last step; lte_lo / lte_hi: the lanes
+    // at or below this one. The elements of step s + 1 were read a step ago (readlane(vn, 0) does
+    // not wait on a fresh read); those of step s + 2 are read now (past the block near its end:
+    // inside the LDS image or beyond it, unused either way).
+    __device__ __forceinline__ void step(const uint8_t *D, uint32_t s, bool fin, uint32_t lane, uint32_t lte_lo,
+                                         uint32_t lte_hi)
     {
-        addr += (s & 1) ? dA - dB : dB;
-        const uint32_t vn = D[addr];  // the next step's element (past the block on the last: unused)
+        addr += (s & 1) ? dB : dA - dB;
+        const uint32_t vnn = D[addr];
         const uint32_t prev = lane_shr1(v, pv);
         const uint32_t nx = dpp<0x130>(v, readlane(vn, 0));  // wave_shl 1: the next element
-        const uint64_t le = ballot(v != prev) & lte;
-        const uint32_t o = le ? lane - (63u - (uint32_t)__builtin_clzll(le)) : po + 1 + lane;
+        const uint64_t st = ballot(v != prev);
+        // the run offset: from the last run start at or below this lane, else the previous step's
+        const uint32_t lo = (uint32_t)st & lte_lo, hi = (uint32_t)(st >> 32) & lte_hi;
+        const uint32_t t = min(ffbh(hi), ffbh(lo) + 32u);  // leading zeros of (hi, lo) when not 0
+        const uint32_t o = (lo | hi) ? lane - 63u + t : po + 1u + lane;
         const uint32_t j = o % 258u;
-        const bool last = fin && lane == 63;
-        const bool end = nx != v || (fin && lane == 62);
-        const uint32_t cnt = last ? 1u : (uint32_t)(j <= 2) + (uint32_t)(j == 257) + (uint32_t)(end && j >= 2 && j <= 256);
-        const uint64_t b1 = ballot(cnt >= 1), b2 = ballot(cnt == 2);
-        const uint64_t pos = q + count_below(b1) + count_below(b2);
-        const uint32_t first = (last || j <= 2) ? v : (j == 257 ? 255u : j - 2);
-        if (cnt >= 1) out[pos] = (uint8_t)first;
-        if (cnt == 2) out[pos + 1] = 0;
-        q += __popcll(b1) + __popcll(b2);
+        const uint64_t lastm = fin ? (1ull << 63) : 0ull;
+        const uint64_t endm = ballot(nx != v) | (fin ? (1ull << 62) : 0ull);
+        const uint64_t lit = ballot(j <= 2) | lastm;
+        const uint64_t e1 = lit | endm | ballot(j == 257);
+        const uint64_t e2 = ballot(j == 2) & endm & ~lastm;
+        const uint32_t pos = q + count_below(e1) + count_below(e2);
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)sel(lit, v, j - 2), rs, (int)sel(e1, pos, kDrop), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)0, rs, (int)sel(e2, pos + 1, kDrop), 0, 0);
+        q += (uint32_t)__builtin_popcountll(e1) + (uint32_t)__builtin_popcountll(e2);
         po = readlane(o, 63);
         pv = readlane(v, 63);
         v = vn;
+        vn = vnn;
     }
 };
 
@@ -1374,31 +1365,47 @@ __device__ __forceinline__ void emit_whole(const uint8_t *D, const uint32_t *a0,
                                            const uint32_t *dB, uint32_t L, uint8_t *const *out, uint32_t lane)
 {
     const uint64_t lte = ~0ull >> (63 - lane);  // lanes at or below this one
+    const uint32_t lte_lo = (uint32_t)lte, lte_hi = (uint32_t)(lte >> 32);
     EmitWhole e[kN];
 #pragma unroll
     for (int k = 0; k < kN; ++k) e[k].init(D, a0[k], dA[k], dB[k], out[k]);
     for (uint32_t base = 0, s = 0; base < L; base += 64, ++s) {
         const bool fin = base + 64 == L;  // (uniform)
 #pragma unroll
-        for (int k = 0; k < kN; ++k) e[k].step(D, s, fin, lane, lte);
+        for (int k = 0; k < kN; ++k) e[k].step(D, s, fin, lane, lte_lo, lte_hi);
     }
 }
 
 // blocks of B <= 128: one workgroup per tile loads it once into LDS (as tile_cost_kernel
 // does), then each wave emits blocks of the tile from LDS
-__global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
+#ifndef HC_EMIT_WPE
+#define HC_EMIT_WPE 7
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE))) void emit_tile_kernel(EncArgs a, Ws ws)
 {
     __shared__ uint8_t D[(kTile + 1) * kDS];
+    __shared__ uint32_t edge[4 * kLU];  // tile_put
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[0];
     const bool diff = a.diff != 0;
-    // (no prefetch of the next tile as in tile_cost_kernel: its registers across the emit loop
-    // cost half the occupancy, measured slower)
+    // the next tile's raw dwords are in flight while this one is emitted (tile_fetch / tile_put,
+    // as in tile_cost_kernel): without the overlap the loads alone took half the kernel's time
+    uint32_t v[kLU];
+    TileAt nx;
+    auto wanted = [&](const TileAt &g) __attribute__((always_inline)) { return g.ok && ws.meta[g.i].B <= kTile; };
+    if (blockIdx.x < ntiles) {
+        nx = tile_at(a, ws, blockIdx.x);
+        if (wanted(nx)) tile_fetch(nx, v, tid);
+    }
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const TileAt g = tile_at(a, ws, t);
-        if (!g.ok || ws.meta[g.i].B > kTile) continue;  // (uniform over the workgroup)
-        load_tile(D, g.mat, g.n, g.W, g.tx0, g.ty0, g.tw, g.th, diff, tid);
-        lds_barrier();
+        const TileAt g = nx;
+        const bool want = wanted(g);
+        if (want) tile_put(D, edge, g, v, diff, tid);  // (its first barrier ends the previous tile)
+        if (t + gridDim.x < ntiles) {
+            nx = tile_at(a, ws, t + gridDim.x);
+            if (wanted(nx)) tile_fetch(nx, v, tid);
+        }
+        if (!want) continue;  // (uniform over the workgroup)
         const uint32_t i = g.i;
         const AMeta &M = ws.meta[i];
         const uint64_t W = g.W, B = M.B, tx0 = g.tx0, ty0 = g.ty0;
@@ -1491,7 +1498,6 @@ __global__ __launch_bounds__(256) void emit_tile_kernel(EncArgs a, Ws ws)
                 }
             }
         }
-        lds_barrier();
     }
 }
 
@@ -2911,13 +2917,18 @@ __device__ __forceinline__ uint64_t revert_block(Read &&read, uint64_t pos, uint
 }
 
 // A wave's window on a symbol stream read in order: the symbols below `hi` (a multiple of 256)
-// sit in a 1 KB LDS ring, the next 256 are in flight in a register (one dword per lane), so the
-// revert's 64-symbol steps read LDS, not HBM.
+// sit in a 1 KB LDS ring, the next kPF x 256 are in flight in registers (one dword per lane
+// each), so the revert's 64-symbol steps read LDS, not HBM, and a refill waits on a load issued
+// kPF refills (4 kPF steps) earlier: with one in flight, the refills waited on HBM latency.
+#ifndef HC_RING_PF
+#define HC_RING_PF 1
+#endif
 struct SymRing {
+    static constexpr uint32_t kPF = HC_RING_PF;
     uint8_t *R;
     const uint32_t *sw;  // the symbols as dwords (the slab is 16-aligned)
     uint64_t nsym, hi;
-    uint32_t pf, lane;
+    uint32_t pf[kPF], lane;
     __device__ __forceinline__ uint32_t fetch(uint64_t at) const
     {
         const uint64_t o = at + 4 * lane;
@@ -2929,20 +2940,23 @@ struct SymRing {
         uint32_t q[4];
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) q[k] = fetch(base + 256 * k);
+        hi = base + 1024;
+#pragma unroll
+        for (uint32_t k = 0; k < kPF; ++k) pf[k] = fetch(hi + 256 * k);
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k)
             *reinterpret_cast<uint32_t *>(R + ((base + 256 * k + 4 * lane) & 1023)) = q[k];
-        hi = base + 1024;
-        pf = fetch(hi);
         __builtin_amdgcn_wave_barrier();
     }
     // symbol p + lane (p + 64 <= hi afterwards; p >= hi - 1024 by construction)
     __device__ __forceinline__ uint32_t operator()(uint64_t p)
     {
         while (p + 64 > hi) {
-            *reinterpret_cast<uint32_t *>(R + ((hi + 4 * lane) & 1023)) = pf;
+            *reinterpret_cast<uint32_t *>(R + ((hi + 4 * lane) & 1023)) = pf[0];
+#pragma unroll
+            for (uint32_t k = 0; k + 1 < kPF; ++k) pf[k] = pf[k + 1];
+            pf[kPF - 1] = fetch(hi + 256 * kPF);
             hi += 256;
-            pf = fetch(hi);
         }
         __builtin_amdgcn_wave_barrier();
         return R[(p + lane) & 1023];
@@ -2952,7 +2966,10 @@ struct SymRing {
 // transform.cpp:191-216 for blocks of B = 8..128 (mode 0): one workgroup per tile; each wave
 // reverts the blocks of one tile block row (one group: they follow each other in the stream)
 // into an LDS image of the tile, which then leaves as whole rows
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void unblock_tile_kernel(DecArgs a, Ws ws)
+#ifndef HC_UNB_WPE
+#define HC_UNB_WPE 7
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_UNB_WPE))) void unblock_tile_kernel(DecArgs a, Ws ws)
 {
     __shared__ uint8_t T[kTile * kDS];
     __shared__ uint32_t ring[4][256];
