@@ -216,6 +216,12 @@ class Batch:
         b = int((self.est != 0).sum() + (self.bst != 0).sum() + (self.blens != self.lens).sum())
         return b + (0 if torch.equal(self.back, self.raw) else 1)
 
+    def fgk_symbols(self):
+        """FGK symbols of the whole batch: every stream's u64 header count (headers.cpp:110-116)"""
+        t = self.torch
+        hdr = self.enc[self.eoffs.view(-1, 1) + t.arange(8, device=self.enc.device)].to(t.int64)
+        return int((hdr << (8 * t.arange(8, device=self.enc.device))).sum())
+
     def encoded(self, k):
         n = int(self.elens[k])
         o = k * self.cap
@@ -260,6 +266,10 @@ def roofline(S, N, enc_bytes, enc_ms, dec_ms, mode, kind):
             pm = json.load(f)
         key = f"{dom}:{mode}:{kind}:{S}"
         e = pm.get("launches", {}).get(key)
+        et = pm.get("launches", {}).get(f"{dom}_tables:{mode}:{kind}:{S}")
+        if e and et:  # the encoder's two mode launches (path cache, level tables) run side by side
+            e = {k: e.get(k, 0) + et.get(k, 0) for k in ("hbm_bytes", "valu_salu_insts")}
+            key += " + " + f"{dom}_tables:{mode}:{kind}:{S}"
         if e and pm.get("source_sha") == src_sha():
             r["traffic"] = e.get("hbm_bytes")
             r["traffic_source"] = f"profiles/pmc_summary.json[{key}] (rocprofv3 PMC, same kernel source)"
@@ -283,7 +293,8 @@ def config_batch(torch, hc, dev, stream, name, what, kind, S, use_diff, steps, d
            "GiBps": round(S * b.N / ((enc_ms + dec_ms) * 1e-3) / 2**30, 4),
            "encode_GiBps": round(S * b.N / (enc_ms * 1e-3) / 2**30, 4),
            "decode_GiBps": round(S * b.N / (dec_ms * 1e-3) / 2**30, 4),
-           "bits_per_byte": round(enc_bytes * 8 / (S * b.N), 4), "round_trip_exact": bad == 0}
+           "bits_per_byte": round(enc_bytes * 8 / (S * b.N), 4), "round_trip_exact": bad == 0,
+           "fgk_symbols_per_stream": round(b.fgk_symbols() / S, 1)}
     # the reference's digests for streams k = 0..3 of this kind (512x512)
     if side == 512 and digests:
         ok = True
@@ -579,6 +590,7 @@ def main():
         "encode_GiBps": round(world * S * N_RAW / (enc_ms * 1e-3) / 2**30, 4),
         "decode_GiBps": round(world * S * N_RAW / (dec_ms * 1e-3) / 2**30, 4),
         "bits_per_byte": round(enc_total * 8 / raw_total, 4), "bit_exact": True,
+        "fgk_symbols_per_stream": round(b.fgk_symbols() / S, 1),
     }
     if world == 1:
         roof["measured_copy_GBps"] = copy_peak(torch, dev, stream)

@@ -2994,17 +2994,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_UNB_WPE)
         rd.sw = reinterpret_cast<const uint32_t *>(sym);
         rd.nsym = M.count;
         rd.lane = lane;
-        for (uint32_t by = wv; by < nby; by += 4) {
-            const uint64_t gby = ty0 / B + by;
-            uint64_t pos = starts[gby * ntx + tix];
+        // all of the wave's rows at once (one HBM round trip, not one per row and value): lane k
+        // the start of row wv + 4 k (its group), lane 16 k + bx the scan order of its block bx
+        uint64_t rpos = 0;
+        uint32_t rh = 0;
+        {
+            const uint32_t k = lane >> 4, bx = lane & 15;
+            if (lane < 4 && wv + 4 * lane < nby) rpos = starts[(ty0 / B + wv + 4 * lane) * ntx + tix];
+            if (wv + 4 * k < nby && bx < nbx) {
+                const uint64_t kl = (ty0 / B + wv + 4 * k) * per_row + tx0 / B + bx;
+                rh = (sym[24 + kl / 8] >> (7 - kl % 8)) & 1;
+            }
+        }
+        for (uint32_t by = wv, k = 0; by < nby; by += 4, ++k) {
+            uint64_t pos = (uint64_t)readlane((uint32_t)rpos, k) | (uint64_t)readlane((uint32_t)(rpos >> 32), k) << 32;
             rd.start(pos);
-            // the row's scan orders, one block per lane (nbx <= 16)
-            const uint64_t kl = gby * per_row + tx0 / B + lane;
-            const uint32_t lane_h = lane < nbx ? (sym[24 + kl / 8] >> (7 - kl % 8)) & 1 : 0u;
             for (uint32_t bx = 0; bx < nbx; ++bx) {
                 const uint32_t x0 = bx * b32, y0 = by * b32;
                 const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
-                const bool horiz = readlane(lane_h, bx) != 0;
+                const bool horiz = readlane(rh, 16 * k + bx) != 0;
                 const uint32_t inner = horiz ? sx : sy;
                 if (sx == b32 && sy == b32) {  // (uniform) a whole block: shifts, B a power of two
                     const uint32_t lg = (uint32_t)__builtin_ctz(b32);

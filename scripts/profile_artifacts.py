@@ -47,8 +47,16 @@ def main():
     ap.add_argument("--streams", type=int, default=65536)
     ap.add_argument("--mode", default="cm")
     ap.add_argument("--kind", default="photo")
-    ap.add_argument("--symbols", type=float, default=201635.0, help="FGK symbols per stream (photo -c -m)")
+    ap.add_argument("--symbols", type=float, default=0.0,
+                    help="FGK symbols per stream (default: fgk_symbols_per_stream of the stats pass's bench line)")
     a = ap.parse_args()
+    if not a.symbols:
+        log = os.path.join(ROOT, "gpurun_out", "prof", f"{a.tag}_stats.log")
+        for line in open(log):
+            if line.startswith("{"):
+                a.symbols = float(json.loads(line)["fgk_symbols_per_stream"])
+        if not a.symbols:
+            raise SystemExit(f"no fgk_symbols_per_stream in {log}: pass --symbols")
     prof = os.path.join(ROOT, "gpurun_out", "prof")
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -95,7 +103,16 @@ def main():
         bench["launches"][f"{name}:{a.mode}:{a.kind}:{a.streams}"] = e
     with open(os.path.join(out, f"{a.round}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    with open(os.path.join(out, "pmc_summary.json"), "w") as f:
+    # other workloads' entries measured on the same source stay (one file, keyed per workload)
+    path = os.path.join(out, "pmc_summary.json")
+    if os.path.exists(path):
+        old = json.load(open(path))
+        if old.get("source_sha") == src:
+            for k, v in old.get("launches", {}).items():
+                bench["launches"].setdefault(k, v)
+    bench["_note"] = ("per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE) and SQ_INSTS_VALU + SQ_INSTS_SALU from "
+                      "rocprofv3 PMC passes, keyed kernel:mode:kind:streams; details in profiles/r*_pmc_summary.json")
+    with open(path, "w") as f:
         json.dump(bench, f, indent=1)
     print(json.dumps(summary["per_symbol"], indent=1))
     print(json.dumps(bench, indent=1))
