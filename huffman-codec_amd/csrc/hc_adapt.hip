@@ -47,6 +47,13 @@ namespace {
 // (load, equality words, candidates, summaries) into g_tc_prof (hc_debug_tc_prof reads it).
 #ifdef HC_TC_PROF
 __device__ unsigned long long g_tc_prof[4];
+#define HC_TC_BEGIN() uint64_t tc_t = __builtin_amdgcn_s_memtime()
+#define HC_TC_MARK(i)                                                                              \
+    do {                                                                                           \
+        const uint64_t tc_n = __builtin_amdgcn_s_memtime();                                        \
+        if (tid == 0) atomicAdd(&g_tc_prof[(i) - 1], (unsigned long long)(tc_n - tc_t));           \
+        tc_t = tc_n;                                                                               \
+    } while (0)
 #else
 #define HC_TC_BEGIN()
 #define HC_TC_MARK(i)
@@ -2072,7 +2079,10 @@ struct BWalk {
 
 // One wave per stream (the streams the parallel pass below does not take): the serial process
 // over the whole stream.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void bounds_kernel(DecArgs a, Ws ws)
+#ifndef HC_BOUNDS_WPE
+#define HC_BOUNDS_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_BOUNDS_WPE))) void bounds_kernel(DecArgs a, Ws ws)
 {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     for (uint32_t i = blockIdx.x * 4 + wv; i < a.n; i += gridDim.x * 4) {
