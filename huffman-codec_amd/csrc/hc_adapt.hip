@@ -76,14 +76,15 @@ struct AMeta {
     uint64_t offs;                   // encode: the winner's u64 block offsets (workspace offset)
     uint64_t slab;                   // first byte of the stream's workspace slab
     uint64_t sym;                    // first symbol byte (workspace offset)
-    uint64_t starts;                 // decode: first group-start entry (workspace offset, bytes)
+    uint64_t starts;                 // decode: first group-start entry (workspace offset, bytes; mode 0: every block's)
     uint64_t csum;                   // decode: first chunk-sum byte (workspace offset)
     uint64_t nb, B, K, groups, chunks, hdr, count;
     uint32_t nc, diff;
     int32_t status;
     uint32_t best;                   // encode: the chosen candidate
-    uint32_t mode;                   // decode: 0 tile groups (B = 8..128, power of 2), 1 one entry
-                                     // per block (B >= 256, power of 2), 2 K-block groups (other B)
+    uint32_t mode;                   // decode: 0 tiles, one entry per block (B = 8..128, power of 2),
+                                     // 1 one entry per block (B >= 256, power of 2), 2 K-block
+                                     // groups (other B)
     uint32_t pad2;
     uint64_t tiles;                  // decode: tiles (mode 0)
     uint64_t ents;                   // decode: group-start entries reserved at `starts`
@@ -1715,9 +1716,9 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
         }
         const bool pow2 = (b & (b - 1)) == 0;
         m.tiles = 0;
-        if (pow2 && b >= 8 && b <= kTile) {  // groups = the block rows of a tile
+        if (pow2 && b >= 8 && b <= kTile) {  // tiles; every block's start is recorded
             m.mode = 0;
-            m.K = kTile / b;
+            m.K = 1;
             m.groups = 0;
             m.tiles = cdiv(w, kTile) * cdiv(h, kTile);
         } else if (pow2 && b > kTile) {
@@ -1731,12 +1732,12 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
             m.K = area >= kGroupBytes ? 1 : cdiv(kGroupBytes, area ? area : 1);
             m.groups = cdiv(nb, m.K);
         }
-        // the group-start entries the bounds pass writes must fit the ones reserved for this
-        // stream (dec_plan: group_entries_bound of the output capacity). Genuine streams always
-        // do (W, H >= 8); a forged header with a matrix 1..7 wide or high can name more tile
-        // block rows than that, and takes K-block groups large enough to fit instead
+        // the group-start entries the bounds pass writes (mode 0: one per block) must fit the
+        // ones reserved for this stream (dec_plan: group_entries_bound of the output capacity).
+        // Genuine streams always do; a forged header with a matrix 1..7 wide or high can name
+        // more blocks than that, and takes K-block groups large enough to fit instead
         const uint64_t room = group_entries_bound(a.out_caps[i]);
-        const uint64_t ents = m.mode == 0 ? cdiv(h, b) * cdiv(w, kTile) : m.groups;
+        const uint64_t ents = m.mode == 0 ? nb : m.groups;
         if (ents > room) {
             const uint64_t bx = b < w ? b : w, by = b < h ? b : h, area = bx * by;
             uint64_t K = area >= kGroupBytes ? 1 : cdiv(kGroupBytes, area ? area : 1);
@@ -1746,7 +1747,7 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
             m.groups = cdiv(nb, K);
             m.tiles = 0;
         }
-        m.ents = m.mode == 0 ? cdiv(h, b) * cdiv(w, kTile) : m.groups;
+        m.ents = m.mode == 0 ? nb : m.groups;
         m.chunks = m.diff ? cdiv(w * h, kChunk) : 0;
         // many block symbols: the parallel boundary pass (the slab holds its data, dec_plan)
         m.par = m.pcap && nb && count - m.hdr >= par_min();
@@ -1883,13 +1884,12 @@ struct BWalk {
     uint64_t nsym;       // symbols (adaptive header included)
     uint64_t hdr;        // first block symbol
     uint64_t *starts;
-    uint64_t K, ents, ntx;
-    bool tiled;
+    uint64_t K, ents;
     uint64_t W, H, B, per_row, nb;  // geometry (Geo geo() for the rest: entries and exits only)
     uint32_t lane;
     // process state
     uint64_t pos, blk, got, want;
-    uint64_t bx, by, kq, gq;  // block column / row; mode 0: bx mod K, bx / K; else blk mod K, blk / K
+    uint64_t bx, by, kq, gq;  // block column / row; blk mod K, blk / K (K = 1 in mode 0: every block)
     uint32_t r, last;
 
     __device__ void init(const AMeta &M, const uint8_t *sym, uint64_t *st, uint32_t l)
@@ -1900,13 +1900,11 @@ struct BWalk {
         starts = st;
         K = M.K;
         ents = M.ents;
-        tiled = M.mode == 0;
         W = M.w;
         H = M.h;
         B = M.B;
         per_row = cdiv(W, B);
         nb = per_row * cdiv(H, B);
-        ntx = cdiv(M.w, kTile);
         lane = l;
     }
     __device__ Geo geo() const
@@ -1919,19 +1917,15 @@ struct BWalk {
     {
         return (W - bx * B < B ? W - bx * B : B) * (H - by * B < B ? H - by * B : B);
     }
-    __device__ uint64_t entry() const { return tiled ? by * ntx + gq : gq; }  // when kq == 0
+    __device__ uint64_t entry() const { return gq; }  // when kq == 0
     // step to the next block; its group-start entry (~0 if it starts no group)
     __device__ uint64_t next_block()
     {
         if (++bx == per_row) {
             bx = 0;
             ++by;
-            if (tiled) kq = gq = 0;
-        } else if (tiled && ++kq == K) {
-            kq = 0;
-            ++gq;
         }
-        if (!tiled && ++kq == K) {
+        if (++kq == K) {
             kq = 0;
             ++gq;
         }
@@ -1960,13 +1954,8 @@ struct BWalk {
         blk = by * per_row + bx;
         got = rel;
         want = block_want();
-        if (tiled) {
-            kq = bx % K;
-            gq = bx / K;
-        } else {
-            kq = blk % K;
-            gq = blk / K;
-        }
+        kq = blk % K;
+        gq = blk / K;
         if (got == 0) {
             r = 0;
             if (kq == 0 && q >= rec_from && lane == 0 && entry() < ents) starts[entry()] = q;
@@ -2958,6 +2947,23 @@ struct SymRing {
             *reinterpret_cast<uint32_t *>(R + ((base + 256 * k + 4 * lane) & 1023)) = q[k];
         __builtin_amdgcn_wave_barrier();
     }
+    // symbols p + 4 lane .. p + 4 lane + 3 as one dword (byte k: symbol p + 4 lane + k), from two
+    // aligned ring dwords (p + 260 <= hi afterwards)
+    __device__ __forceinline__ uint32_t read4(uint64_t p)
+    {
+        while (p + 260 > hi) {
+            *reinterpret_cast<uint32_t *>(R + ((hi + 4 * lane) & 1023)) = pf[0];
+#pragma unroll
+            for (uint32_t k = 0; k + 1 < kPF; ++k) pf[k] = pf[k + 1];
+            pf[kPF - 1] = fetch(hi + 256 * kPF);
+            hi += 256;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t a = (uint32_t)p + 4 * lane;
+        const uint32_t w0 = *reinterpret_cast<const uint32_t *>(R + (a & 1020u));
+        const uint32_t w1 = *reinterpret_cast<const uint32_t *>(R + ((a + 4) & 1020u));
+        return __builtin_amdgcn_alignbyte(w1, w0, a & 3u);
+    }
     // symbol p + lane (p + 64 <= hi afterwards; p >= hi - 1024 by construction)
     __device__ __forceinline__ uint32_t operator()(uint64_t p)
     {
@@ -2973,9 +2979,100 @@ struct SymRing {
     }
 };
 
-// transform.cpp:191-216 for blocks of B = 8..128 (mode 0): one workgroup per tile; each wave
-// reverts the blocks of one tile block row (one group: they follow each other in the stream)
-// into an LDS image of the tile, which then leaves as whole rows
+// transform.cpp:162-187 for a whole block (B a power of two, B x B bytes) of the tile path, 256
+// symbols per step: each lane takes 4 consecutive symbols (one ring dword), composes their
+// transitions, and one wave scan of the composed functions and one of the lanes' output lengths
+// serve all four (64 symbols per step paid two scans and four lane reads per 64). Literals are
+// placed by their lanes (a lane past the block end writes to the image's unused pad byte), each
+// count's run by the whole wave. The bounds pass proved the block whole, so its end lies in the
+// stream and the last step's lanes past it are never placed.
+struct RevChain {
+    SymRing rd;
+    uint64_t pos;
+    uint32_t got, want, r, last;
+    uint32_t tb, sl, so, lg, bm;  // T byte of element q: tb + (q >> lg) * sl + (q & bm) * so
+    __device__ __forceinline__ void begin(uint64_t p, uint32_t b32, uint32_t x0, uint32_t y0, bool horiz)
+    {
+        pos = p;
+        got = 0;
+        want = b32 * b32;
+        r = 0;
+        last = 0;
+        lg = (uint32_t)__builtin_ctz(b32);
+        bm = b32 - 1;
+        sl = horiz ? kDS : 1u;
+        so = horiz ? 1u : kDS;
+        tb = y0 * kDS + x0;
+        rd.start(p);
+    }
+    __device__ __forceinline__ bool live() const { return got < want; }
+    __device__ __forceinline__ void step(uint8_t *T, uint32_t lane)
+    {
+        constexpr uint32_t kPad = kDS - 1;  // row 0's last byte: outside every row's 128 bytes
+        const uint32_t w = rd.read4(pos);
+        uint32_t x[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) x[k] = (w >> (8 * k)) & 255u;
+        const uint32_t p0 = lane_shr1(x[3], last);
+        uint32_t f[4];
+        f[0] = x[0] == p0 ? kFsmEq : kFsmNe;
+#pragma unroll
+        for (uint32_t k = 1; k < 4; ++k) f[k] = x[k] == x[k - 1] ? kFsmEq : kFsmNe;
+        const uint32_t F = fsm_then(f[3], fsm_then(f[2], fsm_then(f[1], f[0])));
+        const uint32_t inc = fsm_scan(F);
+        uint32_t st = fsm_at(lane_shr1(inc, kFsmId), r);
+        uint32_t len[4], val[4], c[4], cum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t pk = k ? x[k - 1] : p0;
+            len[k] = st == 3 ? x[k] : 1u;
+            val[k] = st == 3 ? pk : x[k];
+            cum += len[k];
+            c[k] = cum;
+            st = fsm_at(f[k], st);
+        }
+        const uint32_t acc = wave_sum_incl(cum), base = acc - cum + got;
+        const uint64_t hit = ballot(acc + got >= want);
+        const uint32_t L = hit ? (uint32_t)__builtin_ctzll(hit) : 64u;
+        // in lane L the block's last symbol: the first k whose output reaches `want`
+        const uint32_t kx = base + c[0] >= want ? 0u : base + c[1] >= want ? 1u : base + c[2] >= want ? 2u : 3u;
+        const uint32_t kL = hit ? readlane(kx, L) : 3u;
+        const uint32_t lim = lane < L ? 4u : (lane == L ? kL + 1 : 0u);  // this lane's symbols in the block
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t q = base + c[k] - 1;
+            const bool lit = k < lim && len[k] == 1;
+            T[lit ? tb + (q >> lg) * sl + (q & bm) * so : kPad] = (uint8_t)val[k];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            for (uint64_t runs = ballot(k < lim && len[k] > 1); runs; runs &= runs - 1) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(runs);
+                const uint32_t n = readlane(len[k], l), v = readlane(val[k], l);
+                const uint32_t b = readlane(base + c[k], l) - n;
+                for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+                    const uint32_t q = b + j0 + lane;
+                    T[j0 + lane < n ? tb + (q >> lg) * sl + (q & bm) * so : kPad] = (uint8_t)v;
+                }
+            }
+        }
+        if (hit) {
+            got = want;
+        } else {
+            got += readlane(acc, 63);
+            r = fsm_at(readlane(inc, 63), r);
+            last = readlane(x[3], 63);
+            pos += 256;
+        }
+    }
+};
+
+// transform.cpp:191-216 for blocks of B = 8..128 (mode 0): one workgroup per tile, the blocks
+// reverted into an LDS image of the tile, which then leaves as whole rows. The bounds pass
+// records every block's start (mode 0), so the blocks are independent: wave wv takes blocks
+// wv, wv + 4, .. of the tile (RevChain, 256 symbols per step); their starts and scan orders are
+// loaded in one round trip per tile (lane m: block wv + 4 m). Tiles with partial blocks (matrix
+// edges) take revert_block, one block at a time.
 #ifndef HC_UNB_WPE
 #define HC_UNB_WPE 7
 #endif
@@ -2985,6 +3082,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_UNB_WPE)
     __shared__ uint32_t ring[4][256];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[2];
+    RevChain ca;
+    ca.rd.R = reinterpret_cast<uint8_t *>(ring[wv]);
+    ca.rd.lane = lane;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t i = find_item(ws.idx[2], a.n, t, ws.ctr[8 + 2]);
         const AMeta &M = ws.meta[i];
@@ -2995,51 +3095,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_UNB_WPE)
         const uint32_t tw = (uint32_t)(W - tx0 < kTile ? W - tx0 : kTile);
         const uint32_t th = (uint32_t)(H - ty0 < kTile ? H - ty0 : kTile);
         const uint32_t b32 = (uint32_t)B;
-        const uint32_t nbx = (tw + b32 - 1) / b32, nby = (th + b32 - 1) / b32;
+        const uint32_t nbx = (tw + b32 - 1) / b32, nby = (th + b32 - 1) / b32, nblk = nbx * nby;
         const uint8_t *sym = at<uint8_t>(ws, M.sym);
         const uint64_t *starts = at<uint64_t>(ws, M.starts);
         const uint64_t per_row = cdiv(W, B);
-        SymRing rd;
-        rd.R = reinterpret_cast<uint8_t *>(ring[wv]);
-        rd.sw = reinterpret_cast<const uint32_t *>(sym);
-        rd.nsym = M.count;
-        rd.lane = lane;
-        // all of the wave's rows at once (one HBM round trip, not one per row and value): lane k
-        // the start of row wv + 4 k (its group), lane 16 k + bx the scan order of its block bx
-        uint64_t rpos = 0;
-        uint32_t rh = 0;
+        // The wave's blocks wv, wv + 4, .. (lane m: block wv + 4 m, <= 64 of them): each lane loads
+        // its block's start and scan order, one round trip per tile. (Whole block rows per wave,
+        // one ring fill per row, measured slower: 3.53 vs 3.33 ms on A512.)
+        auto block_of = [&](uint32_t m, uint32_t &by, uint32_t &bx) __attribute__((always_inline)) {
+            const uint32_t b = wv + 4 * m;
+            by = b / nbx;
+            bx = b - by * nbx;
+        };
+        uint64_t bpos = 0;
+        uint32_t bh = 0;
         {
-            const uint32_t k = lane >> 4, bx = lane & 15;
-            if (lane < 4 && wv + 4 * lane < nby) rpos = starts[(ty0 / B + wv + 4 * lane) * ntx + tix];
-            if (wv + 4 * k < nby && bx < nbx) {
-                const uint64_t kl = (ty0 / B + wv + 4 * k) * per_row + tx0 / B + bx;
-                rh = (sym[24 + kl / 8] >> (7 - kl % 8)) & 1;
+            uint32_t by, bx;
+            block_of(lane, by, bx);
+            if (by < nby) {
+                const uint64_t kl = (ty0 / B + by) * per_row + tx0 / B + bx;
+                bpos = starts[kl];
+                bh = (sym[24 + kl / 8] >> (7 - kl % 8)) & 1;
             }
         }
-        for (uint32_t by = wv, k = 0; by < nby; by += 4, ++k) {
-            uint64_t pos = (uint64_t)readlane((uint32_t)rpos, k) | (uint64_t)readlane((uint32_t)(rpos >> 32), k) << 32;
-            rd.start(pos);
-            for (uint32_t bx = 0; bx < nbx; ++bx) {
+        auto pos_of = [&](uint32_t m) __attribute__((always_inline)) {
+            return (uint64_t)readlane((uint32_t)bpos, m) | (uint64_t)readlane((uint32_t)(bpos >> 32), m) << 32;
+        };
+        ca.rd.sw = reinterpret_cast<const uint32_t *>(sym);
+        ca.rd.nsym = M.count;
+        const uint32_t nm = nblk > wv ? (nblk - wv + 3) / 4 : 0u;
+        if (tw % b32 == 0 && th % b32 == 0) {  // (uniform) whole blocks only
+            for (uint32_t m = 0; m < nm; ++m) {
+                uint32_t by, bx;
+                block_of(m, by, bx);
+                ca.begin(pos_of(m), b32, bx * b32, by * b32, readlane(bh, m) != 0);
+                while (ca.live()) ca.step(T, lane);
+            }
+        } else {
+            SymRing &rd = ca.rd;
+            for (uint32_t m = 0; m < nm; ++m) {
+                uint32_t by, bx;
+                block_of(m, by, bx);
                 const uint32_t x0 = bx * b32, y0 = by * b32;
                 const uint32_t sx = tw - x0 < b32 ? tw - x0 : b32, sy = th - y0 < b32 ? th - y0 : b32;
-                const bool horiz = readlane(rh, 16 * k + bx) != 0;
+                const bool horiz = readlane(bh, m) != 0;
                 const uint32_t inner = horiz ? sx : sy;
-                if (sx == b32 && sy == b32) {  // (uniform) a whole block: shifts, B a power of two
-                    const uint32_t lg = (uint32_t)__builtin_ctz(b32);
-                    // element q -> line q >> lg, offset q & (B - 1): T byte base + line * sl + offset * so
-                    const uint32_t sl = horiz ? kDS : 1u, so = horiz ? 1u : kDS, tb = y0 * kDS + x0;
-                    auto place = [&](uint32_t q, uint32_t v) {
-                        T[tb + ((uint32_t)q >> lg) * sl + ((uint32_t)q & (b32 - 1)) * so] = (uint8_t)v;
-                    };
-                    pos = revert_block<uint32_t>(rd, pos, M.count, b32 * b32, place, lane);
-                } else {
-                    const float inv = 1.0f / (float)inner;
-                    auto place = [&](uint32_t q, uint32_t v) {
-                        const uint32_t a1 = div_small((uint32_t)q, inner, inv), b1 = (uint32_t)q - a1 * inner;
-                        T[(y0 + (horiz ? a1 : b1)) * kDS + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
-                    };
-                    pos = revert_block<uint32_t>(rd, pos, M.count, sx * sy, place, lane);
-                }
+                const uint64_t pos = pos_of(m);
+                rd.start(pos);
+                const float inv = 1.0f / (float)inner;
+                auto place = [&](uint32_t q, uint32_t v) {
+                    const uint32_t a1 = div_small((uint32_t)q, inner, inv), b1 = (uint32_t)q - a1 * inner;
+                    T[(y0 + (horiz ? a1 : b1)) * kDS + x0 + (horiz ? b1 : a1)] = (uint8_t)v;
+                };
+                revert_block<uint32_t>(rd, pos, M.count, sx * sy, place, lane);
             }
         }
         lds_barrier();
