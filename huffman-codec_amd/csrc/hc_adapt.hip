@@ -820,7 +820,7 @@ __device__ __forceinline__ void stats128(const uint64_t *E, const uint64_t *WM, 
 // tiles, the run-segment monoid on partial ones) into the cost words and per-candidate totals,
 // 4. the tile row / column summaries the blocks of B >= 256 are joined from (big_cost_kernel).
 #ifndef HC_TC_WPE
-#define HC_TC_WPE 4
+#define HC_TC_WPE 5
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))) void tile_cost_kernel(EncArgs a, Ws ws)
 {
@@ -1384,10 +1384,115 @@ __device__ __forceinline__ void emit_whole(const uint8_t *D, const uint32_t *a0,
     }
 }
 
+// emit_whole for B >= 16 (L = B * B a multiple of 256): 256 elements per step, 4 consecutive
+// elements of the scan per lane (one LDS dword along a line, four bytes down a column), so the
+// scans and lane reads of a step serve four elements. The run offset mod 258 (all the rules
+// need) comes from a max-scan of the lanes' last run starts (biased element positions; the
+// previous step's run enters as position -(j + 1) with j its last element's offset mod 258),
+// then steps along the lane's elements; each lane emits 0..8 bytes at its exclusive prefix of
+// the counts (one wave sum). Rules as EmitWhole.
+struct EmitWhole4 {
+    static constexpr uint32_t kBias = 512;
+    // the read-ahead past a block's end stays inside the image (the last legal reads: a line's
+    // dword at 128 kDS + 128, a column's 4 bytes from 125 kDS + 131)
+    static constexpr uint32_t kMaxH = kTile * kDS + kTile, kMaxV = (kTile + 1) * kDS - 1 - 3 * kDS;
+    uint32_t addr, dS, pv, po, q, v, vn;
+    bool horiz;
+    rsrc_t rs;
+    __device__ __forceinline__ uint32_t load(const uint8_t *D, uint32_t a) const
+    {
+        if (horiz) return *reinterpret_cast<const uint32_t *>(D + (a < kMaxH ? a : kMaxH));
+        a = a < kMaxV ? a : kMaxV;
+        return (uint32_t)D[a] | (uint32_t)D[a + kDS] << 8 | (uint32_t)D[a + 2 * kDS] << 16 | (uint32_t)D[a + 3 * kDS] << 24;
+    }
+    // a0: this lane's first element of the block (element 4 lane); dS: the step's address increment
+    __device__ __forceinline__ void init(const uint8_t *D, uint32_t a0, uint32_t dS_, bool h, uint8_t *o)
+    {
+        horiz = h;
+        addr = a0 + dS_;
+        dS = dS_;
+        pv = 0x100;  // differs from every byte: element 0 starts a run
+        po = 0;
+        q = 0;
+        rs = out_rsrc(o);
+        v = load(D, a0);
+        vn = load(D, addr);
+    }
+    __device__ __forceinline__ void step(const uint8_t *D, bool fin, uint32_t lane)
+    {
+        addr += dS;
+        const uint32_t vnn = load(D, addr);  // two steps ahead
+        uint32_t x[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) x[k] = (v >> (8 * k)) & 255u;
+        const uint32_t p0 = lane_shr1(x[3], pv);
+        bool S[4];
+        S[0] = x[0] != p0;
+#pragma unroll
+        for (uint32_t k = 1; k < 4; ++k) S[k] = x[k] != x[k - 1];
+        // the last run start at or below each lane (biased element position of the step)
+        const uint32_t lastk = S[3] ? 3u : S[2] ? 2u : S[1] ? 1u : 0u;
+        const uint32_t A = (S[0] | S[1] | S[2] | S[3]) ? 4 * lane + lastk + kBias : 0u;
+        const uint32_t M = wave_scan(A, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+        uint32_t Mx = lane_shr1(M, 0u);
+        const uint32_t Cb = kBias - (po + 1);  // the previous step's run
+        Mx = Mx > Cb ? Mx : Cb;
+        uint32_t j[4];
+        j[0] = S[0] ? 0u : (4 * lane + kBias - Mx) % 258u;
+#pragma unroll
+        for (uint32_t k = 1; k < 4; ++k) j[k] = S[k] ? 0u : (j[k - 1] == 257u ? 0u : j[k - 1] + 1);
+        // run ends: the next element differs (lane 63's next is the next step's first)
+        const uint32_t nx0 = dpp<0x130>(x[0], readlane(vn, 0) & 255u);  // wave_shl 1
+        const bool f63 = fin && lane == 63;
+        bool end[4];
+        end[0] = S[1];
+        end[1] = S[2];
+        end[2] = S[3] || f63;  // before the block's last element
+        end[3] = nx0 != x[3];
+        uint32_t cnt = 0, e1[4], e2[4], first[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const bool last = k == 3 && f63;
+            const bool lit = j[k] <= 2 || last;
+            e1[k] = (lit || end[k] || j[k] == 257u) ? 1u : 0u;
+            e2[k] = (j[k] == 2u && end[k] && !last) ? 1u : 0u;
+            first[k] = lit ? x[k] : j[k] - 2;
+            cnt += e1[k] + e2[k];
+        }
+        const uint32_t incl = wave_sum_incl(cnt);
+        uint32_t off = q + incl - cnt;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)first[k], rs, (int)(e1[k] ? off : kDrop), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)0, rs, (int)(e2[k] ? off + 1 : kDrop), 0, 0);
+            off += e1[k] + e2[k];
+        }
+        q += readlane(incl, 63);
+        po = readlane(j[3], 63);
+        pv = readlane(x[3], 63);
+        v = vn;
+        vn = vnn;
+    }
+};
+
+template <int kN>
+__device__ __forceinline__ void emit_whole4(const uint8_t *D, const uint32_t *a0, const uint32_t *dS, const bool *horiz,
+                                            uint32_t L, uint8_t *const *out, uint32_t lane)
+{
+    EmitWhole4 e[kN];
+#pragma unroll
+    for (int k = 0; k < kN; ++k) e[k].init(D, a0[k], dS[k], horiz[k], out[k]);
+    for (uint32_t base = 0; base < L; base += 256) {
+        const bool fin = base + 256 == L;  // (uniform)
+#pragma unroll
+        for (int k = 0; k < kN; ++k) e[k].step(D, fin, lane);
+    }
+}
+
 // blocks of B <= 128: one workgroup per tile loads it once into LDS (as tile_cost_kernel
 // does), then each wave emits blocks of the tile from LDS
 #ifndef HC_EMIT_WPE
-#define HC_EMIT_WPE 7
+#define HC_EMIT_WPE 6
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE))) void emit_tile_kernel(EncArgs a, Ws ws)
 {
@@ -1461,14 +1566,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE
             // inside one 64-block fetch since m steps by 2; four at a time measured slower: SGPRs)
             auto group = [&](auto nn, uint32_t b, uint32_t m) __attribute__((always_inline)) {
                 constexpr int kN = decltype(nn)::value;
-                uint32_t a0[kN], dA[kN], dB[kN];
                 uint8_t *out[kN];
 #pragma unroll
-                for (int k = 0; k < kN; ++k) {
-                    whole_at(b + 4 * k, readlane(lane_h, m + k) != 0, a0[k], dA[k], dB[k]);
-                    out[k] = out_of(m + k);
+                for (int k = 0; k < kN; ++k) out[k] = out_of(m + k);
+                if (b32 >= 16) {  // (uniform) 4 elements per lane: element 4 lane's address, per step +dS
+                    uint32_t a0[kN], dS[kN];
+                    bool hz[kN];
+                    const uint32_t p = 4 * lane, ln = p >> lg, of = p & (b32 - 1);
+#pragma unroll
+                    for (int k = 0; k < kN; ++k) {
+                        const uint32_t bb = b + 4 * k, x0 = (bb % nbx) * b32, y0 = (bb / nbx) * b32;
+                        hz[k] = readlane(lane_h, m + k) != 0;
+                        a0[k] = hz[k] ? (y0 + 1 + ln) * kDS + x0 + 4 + of : (y0 + 1 + of) * kDS + x0 + 4 + ln;
+                        dS[k] = hz[k] ? (256u >> lg) * kDS : 256u >> lg;
+                    }
+                    emit_whole4<kN>(D, a0, dS, hz, b32 * b32, out, lane);
+                } else {
+                    uint32_t a0[kN], dA[kN], dB[kN];
+#pragma unroll
+                    for (int k = 0; k < kN; ++k) whole_at(b + 4 * k, readlane(lane_h, m + k) != 0, a0[k], dA[k], dB[k]);
+                    emit_whole<kN>(D, a0, dA, dB, b32 * b32, out, lane);
                 }
-                emit_whole<kN>(D, a0, dA, dB, b32 * b32, out, lane);
             };
             for (uint32_t b = wv; b < nblk;) {
                 const uint32_t m = ((b - wv) >> 2) & 63;
@@ -1868,14 +1986,14 @@ struct Geo {
 
 // The serial boundary process of one stream (transform.cpp:330-361 running revertRLEBlock,
 // transform.cpp:162-187, block by block), from any entry: symbols from `pos` in machine state r
-// at output offset E(blk) + got. One wave, 512 symbols per step (8 per lane, from dword loads
+// at output offset E(blk) + got. One wave, 256 symbols per step (4 per lane, from dword loads
 // re-aligned by v_alignbyte, the next step's already in flight); a scan of the transition
 // functions gives each symbol's state, hence its output length (count: the symbol, literal: 1);
 // a scan of lengths finds the first symbol where the block's byte count is reached. A block that
 // ends inside the step re-scans the rest of the same registers from state 0. The start of every
 // K-th block (group) at or after `rec_from` is recorded for the unblock waves.
 #ifndef HC_BOUNDS_W
-#define HC_BOUNDS_W 2
+#define HC_BOUNDS_W 1
 #endif
 constexpr uint32_t kBW = HC_BOUNDS_W;   // symbol dwords per lane and step
 constexpr uint32_t kBStep = 256 * kBW;  // symbols per step
@@ -2069,7 +2187,7 @@ struct BWalk {
 // One wave per stream (the streams the parallel pass below does not take): the serial process
 // over the whole stream.
 #ifndef HC_BOUNDS_WPE
-#define HC_BOUNDS_WPE 4
+#define HC_BOUNDS_WPE 6
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_BOUNDS_WPE))) void bounds_kernel(DecArgs a, Ws ws)
 {

@@ -37,12 +37,18 @@ def main():
         hc.use_debug_build(True)
         b = bench.AdaptBatch(torch, hc, dev, "photo", args.streams, not args.no_diff, args.side)
         times = {}
-        for _ in range(args.reps):
-            st = bench.adapt_stages(torch, hc, b, stream)
-            hc.DBG_LIB_PATH = path  # (adapt_stages switches back to LIB_PATH, the same file)
-            for direction in ("encode", "decode"):
-                for name, e in st[direction].items():
-                    times.setdefault((direction, name), []).append(e["ms"])
+        try:
+            for _ in range(args.reps):
+                st = bench.adapt_stages(torch, hc, b, stream)
+                hc.DBG_LIB_PATH = path  # (adapt_stages switches back to LIB_PATH, the same file)
+                for direction in ("encode", "decode"):
+                    for name, e in st[direction].items():
+                        times.setdefault((direction, name), []).append(e["ms"])
+        except Exception as ex:  # (a broken variant: report it, go on with the next)
+            print(f"{d}: FAILED {type(ex).__name__}: {ex}", flush=True)
+            del b
+            torch.cuda.empty_cache()
+            continue
         torch.cuda.synchronize(dev)
         enc_sig = (int(b.elens.sum()), int(b.est.abs().sum()),
                    int((b.enc.to(torch.int64) * (torch.arange(b.enc.numel(), device=dev) % 251 + 1)).sum()))
