@@ -530,6 +530,21 @@ struct TileWalk {
     }
 };
 
+// The tile a persistent workgroup's loop index u stands for. Workgroups are dealt round-robin
+// over the 8 XCDs (each with its own L2): in each round of G = gridDim.x tiles, the workgroups
+// of one XCD (b, b + 8, ..) take a contiguous run of G / 8 tiles, so a tile and its left /
+// right neighbours -- whose loads share the 128-byte lines at the tile's edges, and the row
+// above -- mostly meet in one L2 (the identity in a last, partial round).
+#ifndef HC_XCD
+#define HC_XCD 1
+#endif
+__device__ __forceinline__ uint64_t xcd_tile(uint64_t u, uint64_t G, uint64_t n)
+{
+    const uint64_t r = u / G, b = u - r * G, base = r * G;
+    if (!HC_XCD || (G & 7) || base + G > n) return u;
+    return base + (b & 7) * (G >> 3) + (b >> 3);
+}
+
 // A tile of the work list (one workgroup's unit in tile_cost / emit_tile): its matrix and place.
 struct TileAt {
     uint32_t i;            // matrix
@@ -839,7 +854,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
     uint32_t v[kLU];
     TileAt nx;
     if (blockIdx.x < ntiles) {
-        nx = tile_at(a, ws, blockIdx.x);
+        nx = tile_at(a, ws, xcd_tile(blockIdx.x, gridDim.x, ntiles));
         if (nx.ok) tile_fetch(nx, v, tid);
     }
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -850,7 +865,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
         // 1. the tile plus one row above and one column to the left, diff model applied
         if (g.ok) tile_put(D, edge, g, v, diff, tid);
         if (t + gridDim.x < ntiles) {
-            nx = tile_at(a, ws, t + gridDim.x);
+            nx = tile_at(a, ws, xcd_tile(t + gridDim.x, gridDim.x, ntiles));
             if (nx.ok) tile_fetch(nx, v, tid);
         }
         if (!g.ok) continue;  // (uniform over the workgroup)
@@ -1507,7 +1522,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE
     TileAt nx;
     auto wanted = [&](const TileAt &g) __attribute__((always_inline)) { return g.ok && ws.meta[g.i].B <= kTile; };
     if (blockIdx.x < ntiles) {
-        nx = tile_at(a, ws, blockIdx.x);
+        nx = tile_at(a, ws, xcd_tile(blockIdx.x, gridDim.x, ntiles));
         if (wanted(nx)) tile_fetch(nx, v, tid);
     }
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -1515,7 +1530,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE
         const bool want = wanted(g);
         if (want) tile_put(D, edge, g, v, diff, tid);  // (its first barrier ends the previous tile)
         if (t + gridDim.x < ntiles) {
-            nx = tile_at(a, ws, t + gridDim.x);
+            nx = tile_at(a, ws, xcd_tile(t + gridDim.x, gridDim.x, ntiles));
             if (wanted(nx)) tile_fetch(nx, v, tid);
         }
         if (!want) continue;  // (uniform over the workgroup)
