@@ -1701,7 +1701,10 @@ struct DecArgs {
 
 constexpr uint32_t kSub = 2048;        // symbols per sub-chunk
 constexpr uint32_t kSubPerChunk = 8;   // sub-chunks per walked chunk (16384 symbols)
-constexpr uint32_t kZcap = 512;        // Z entries a sub-chunk keeps (more: every symbol is tested)
+#ifndef HC_ZCAP
+#define HC_ZCAP 1024
+#endif
+constexpr uint32_t kZcap = HC_ZCAP;     // Z entries a sub-chunk keeps (more: every symbol is tested; 512: C4m 5.6 ms, 1024: 3.0)
 constexpr uint32_t kWinLook = 64;      // par_z: a reset machine must rejoin s0 within this
 constexpr uint32_t kWinCap = 4096;     // par_scan: a longer window falls back to the serial pass
 constexpr uint64_t kParMin = 1ull << 20;  // block symbols from which a stream takes this pass
@@ -3527,10 +3530,11 @@ uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t
 {
     // symbols <= 8 per payload byte (+64 slack); u64 block starts <= 8 (out_cap / 32 + 16) (see
     // group_entries_bound); chunk sums out_cap / 16384
-    // + the parallel boundary pass: <= 2.26 bytes per symbol of the streams that take it (Z
-    // entries and their window info 2, packed s0 0.25, records) and 4672 bytes of rounding per
-    // stream
-    return ws_header(n) + 27 * total_in + total_out / 4 + total_out / kChunk + 4992ull * n + 4096;
+    // + the parallel boundary pass: per symbol of the streams that take it, the Z entries and
+    // their window info (8 kZcap / kSub bytes: 2 at kZcap 512), packed s0 0.25, records; 4672
+    // bytes of rounding per stream
+    constexpr uint64_t kPar8 = (8 * (8 * kZcap + kSub / 4 + 64) + kSub - 1) / kSub;  // per 8 symbols
+    return ws_header(n) + (8 + kPar8) * total_in + total_out / 4 + total_out / kChunk + 4992ull * n + 4096;
 }
 
 // Diagnostic stage clock (debug build only, hc_debug_stage_clock / hc_debug_stage_times): when
