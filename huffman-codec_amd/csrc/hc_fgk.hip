@@ -565,8 +565,11 @@ struct Fgk {
         if constexpr (kWide) {
             *(inner ? &T.up[c] : scr16()) = (uint16_t)pos;
         } else {
+            // the parent field, in place: LDS and / or without return (no read round trip; this
+            // wave's later LDS reads come after them in order)
             uint32_t *q = inner ? &T.wt[c] : scr32();
-            *q = (*q & ~1023u) | pos;
+            __hip_atomic_fetch_and(q, ~1023u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_or(q, pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
         __builtin_amdgcn_wave_barrier();
     }
