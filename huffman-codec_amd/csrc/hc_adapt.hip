@@ -878,6 +878,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
         const TileAt g = nx;
         const uint32_t i = g.i;
         AMeta &M = ws.meta[i];
+        // read once, before the tile's atomics (after them the compiler must reload from memory)
+        const uint32_t nc = M.nc;
+        const uint64_t pieces = M.pieces;
         HC_TC_BEGIN();
         // 1. the tile plus one row above and one column to the left, diff model applied
         if (g.ok) tile_put(D, edge, g, v, diff, tid);
@@ -935,12 +938,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
             if (whole) wrap_masks(D, WM, wv, lane);
         }
         lds_barrier();
-        const uint64_t *Eh = E, *Ev = E + 2 * kTile;
+        // (Eh / Ev by index into E, never as a selected pointer: a select of the two became a
+        // scratch-memory pointer table and flat loads)
+        constexpr uint32_t kEv = 2 * kTile;
         HC_TC_MARK(2);
         // 3. blocks of B <= 128, both scan orders
         //    (one copy per candidate: B, the lines per word and the group sizes are constants, so
         //    each thread's LDS reads unroll and issue together)
-        const uint32_t nct = M.nc < kTileCand ? M.nc : kTileCand;
+        const uint32_t nct = nc < kTileCand ? nc : kTileCand;
         uint32_t tot[kTileCand] = {};  // this thread's share of each candidate's total
         auto candidate = [&](auto cc) __attribute__((always_inline)) {
             constexpr uint32_t c = decltype(cc)::value;
@@ -962,7 +967,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
                 const uint32_t x0 = bx << lg, y0 = by << lg;
                 uint64_t word = 0;
                 if (it < 2 * nwords) {
-                    const uint64_t *E2 = o ? Ev : Eh;
+                    const uint32_t e2 = o ? kEv : 0u;
                     const uint32_t l0 = o ? x0 : y0, c0 = o ? y0 : x0;  // first line, offset in it
                     if constexpr (B <= 64) {
                         constexpr uint32_t lpw = 64 >> lg;
@@ -971,7 +976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
 #pragma unroll
                         for (uint32_t q = 0; q < lpw; ++q) {
                             const uint32_t r = r0 + q;
-                            uint64_t bits = (E2[2 * (l0 + r) + (c0 >> 6)] >> (c0 & 63)) & msk & ~1ull;
+                            uint64_t bits = (E[e2 + 2 * (l0 + r) + (c0 >> 6)] >> (c0 & 63)) & msk & ~1ull;
                             if (r) {  // the scan's step across the line wrap (transform.cpp:66-94)
                                 const bool eq = o ? DT(y0 + 1, x0 + r) == DT(y0 + B, (int)(x0 + r) - 1)
                                                   : DT(y0 + r + 1, x0) == DT(y0 + r, x0 + B - 1);
@@ -981,7 +986,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
                         }
                     } else {  // B = 128 (x0 = y0 = 0): word j = half j & 1 of line j >> 1
                         const uint32_t r = j >> 1;
-                        word = E2[2 * r + (j & 1)];
+                        word = E[e2 + 2 * r + (j & 1)];
                         if ((j & 1) == 0) {
                             word &= ~1ull;
                             if (r) word |= o ? DT(1, r) == DT(B, (int)r - 1) : DT(r + 1, 0) == DT(r, B - 1);
@@ -1010,12 +1015,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
                         const uint32_t y = y0 + r;
                         const uint32_t first =
                             r ? (uint32_t)(DT(y + 1, x0) == DT(y, x0 + sx - 1)) : 0u;
-                        s = seg_piece(Eh + 2 * y, x0, sx, first);
+                        s = seg_piece(E + 2 * y, x0, sx, first);
                     } else if (o == 1 && r < sx) {  // block column r (vertical)
                         const uint32_t x = x0 + r;
                         const uint32_t first =
                             r ? (uint32_t)(DT(y0 + 1, x) == DT(y0 + sy, (int)x - 1)) : 0u;
-                        s = seg_piece(Ev + 2 * x, y0, sy, first);
+                        s = seg_piece(E + kEv + 2 * x, y0, sy, first);
                     }
                 }
                 s = seg_group(s, B < 64 ? B : 64u, lane);
@@ -1105,11 +1110,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
         }
         HC_TC_MARK(3);
         // 4. tile summaries for the blocks of B >= 256
-        if (M.nc > kTileCand) {
+        if (nc > kTileCand) {
             const uint64_t nty = cdiv(H, kTile);
-            uint64_t *pc = at<uint64_t>(ws, M.pieces);
+            uint64_t *pc = at<uint64_t>(ws, pieces);
             if (tid < th) {
-                const uint64_t *w = Eh + 2 * tid;
+                const uint64_t *w = E + 2 * tid;
                 const Seg s = tw > 1 ? (tw > 64 ? seg_join(seg_leaf(w[0] >> 1, 63), seg_leaf(w[1], tw - 64))
                                                 : seg_leaf(w[0] >> 1, tw - 1))
                                      : seg_id();
@@ -1117,7 +1122,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
                     piece_pack(s, (uint32_t)(w[0] & 1), DT(tid + 1, 0), DT(tid + 1, tw - 1));
             } else if (tid >= 128 && tid - 128 < tw) {
                 const uint32_t x = tid - 128;
-                const uint64_t *w = Ev + 2 * x;
+                const uint64_t *w = E + kEv + 2 * x;
                 const Seg s = th > 1 ? (th > 64 ? seg_join(seg_leaf(w[0] >> 1, 63), seg_leaf(w[1], th - 64))
                                                 : seg_leaf(w[0] >> 1, th - 1))
                                      : seg_id();
