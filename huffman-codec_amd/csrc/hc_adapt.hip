@@ -1280,6 +1280,10 @@ __device__ __forceinline__ uint32_t div_small(uint32_t q, uint32_t d, float inv)
 // starts (carried across steps), j = o mod 258; it emits its byte for j <= 2, 255 at j = 257,
 // the count j - 2 where its run ends (3 <= j + 1 <= 257), and the block's last element is a
 // literal. Byte offsets: popcounts of two ballots. value(p) = the p-th element in scan order.
+// o mod 258 for o < 516 (run offsets: at most the previous step's offset mod 258 plus 258;
+// v_mul_hi_u32 and v_mul_lo_u32 of a division by the constant issue at a quarter of the rate)
+__device__ __forceinline__ uint32_t mod258(uint32_t o) { return o >= 258u ? o - 258u : o; }
+
 template <class Value>
 __device__ __forceinline__ void emit_block(Value value, uint32_t L, uint8_t *out, uint32_t lane)
 {
@@ -1299,7 +1303,7 @@ __device__ __forceinline__ void emit_block(Value value, uint32_t L, uint8_t *out
         const uint64_t sm = ballot(valid && start);
         const uint64_t le = sm & (lt | (1ull << lane));
         const uint32_t o = le ? lane - (63u - (uint32_t)__builtin_clzll(le)) : po + 1 + lane;
-        const uint32_t j = o % 258u;
+        const uint32_t j = mod258(o);
         const bool last = p + 1 == L;
         const bool end = p + 2 == L || (p + 2 < L && nx != v);
         uint32_t cnt = last ? 1u : (uint32_t)(j <= 2) + (uint32_t)(j == 257) + (uint32_t)(end && j >= 2 && j <= 256);
@@ -1310,7 +1314,7 @@ __device__ __forceinline__ void emit_block(Value value, uint32_t L, uint8_t *out
         if (cnt >= 1) out[pos] = (uint8_t)first;
         if (cnt == 2) out[pos + 1] = 0;
         q += __popcll(b1) + __popcll(b2);
-        po = readlane(o, 63);
+        po = readlane(j, 63);  // (mod 258: o itself grows along a long run)
         pv = readlane(v, 63);
         v = vn;
     }
@@ -1387,7 +1391,7 @@ struct EmitWhole {
         const uint32_t lo = (uint32_t)st & lte_lo, hi = (uint32_t)(st >> 32) & lte_hi;
         const uint32_t t = min(ffbh(hi), ffbh(lo) + 32u);  // leading zeros of (hi, lo) when not 0
         const uint32_t o = (lo | hi) ? lane - 63u + t : po + 1u + lane;
-        const uint32_t j = o % 258u;
+        const uint32_t j = mod258(o);
         const uint64_t lastm = fin ? (1ull << 63) : 0ull;
         const uint64_t endm = ballot(nx != v) | (fin ? (1ull << 62) : 0ull);
         const uint64_t lit = ballot(j <= 2) | lastm;
@@ -1397,7 +1401,7 @@ struct EmitWhole {
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)sel(lit, v, j - 2), rs, (int)sel(e1, pos, kDrop), 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)0, rs, (int)sel(e2, pos + 1, kDrop), 0, 0);
         q += (uint32_t)__builtin_popcountll(e1) + (uint32_t)__builtin_popcountll(e2);
-        po = readlane(o, 63);
+        po = readlane(j, 63);  // (mod 258: o itself grows along a long run)
         pv = readlane(v, 63);
         v = vn;
         vn = vnn;
@@ -1475,7 +1479,7 @@ struct EmitWhole4 {
         const uint32_t Cb = kBias - (po + 1);  // the previous step's run
         Mx = Mx > Cb ? Mx : Cb;
         uint32_t j[4];
-        j[0] = S[0] ? 0u : (4 * lane + kBias - Mx) % 258u;
+        j[0] = S[0] ? 0u : mod258(4 * lane + kBias - Mx);  // in 1 .. 510
 #pragma unroll
         for (uint32_t k = 1; k < 4; ++k) j[k] = S[k] ? 0u : (j[k - 1] == 257u ? 0u : j[k - 1] + 1);
         // run ends: the next element differs (lane 63's next is the next step's first)
@@ -3148,9 +3152,12 @@ struct SymRing {
 // stream and the last step's lanes past it are never placed.
 struct RevChain {
     SymRing rd;
+    uint32_t *Mk;  // the wave's 128 run marks (64 + a discard slot per lane)
     uint64_t pos;
     uint32_t got, want, r, last;
     uint32_t tb, sl, so, lg, bm;  // T byte of element q: tb + (q >> lg) * sl + (q & bm) * so
+    // (24-bit multiplies: v_mul_lo_u32 issues at a quarter of the rate, 8 of them per step)
+    __device__ __forceinline__ uint32_t at(uint32_t q) const { return tb + __umul24(q >> lg, sl) + __umul24(q & bm, so); }
     __device__ __forceinline__ void begin(uint64_t p, uint32_t b32, uint32_t x0, uint32_t y0, bool horiz)
     {
         pos = p;
@@ -3202,18 +3209,36 @@ struct RevChain {
         for (uint32_t k = 0; k < 4; ++k) {
             const uint32_t q = base + c[k] - 1;
             const bool lit = k < lim && len[k] == 1;
-            T[lit ? tb + (q >> lg) * sl + (q & bm) * so : kPad] = (uint8_t)val[k];
+            T[lit ? at(q) : kPad] = (uint8_t)val[k];
         }
+        // Runs, all of the step's at once. A count follows three literals, so counts sit >= 4
+        // symbols apart: a lane holds at most one (rl bytes of rv from block byte rq). Lane j of a
+        // 64-byte chunk of the runs' concatenated bytes (run space) takes the run that starts last
+        // at or before it: each run marks its start with key (rq - rs) << 8 | rv, rs its run-space
+        // start, and a max-scan of the marks finds it (the keys grow with the runs: >= 3 literal
+        // bytes lie between two runs), the byte then sits at block byte j + (key >> 8).
+        uint32_t rl = 0, rq = 0, rv = 0;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
-            for (uint64_t runs = ballot(k < lim && len[k] > 1); runs; runs &= runs - 1) {
-                const uint32_t l = (uint32_t)__builtin_ctzll(runs);
-                const uint32_t n = readlane(len[k], l), v = readlane(val[k], l);
-                const uint32_t b = readlane(base + c[k], l) - n;
-                for (uint32_t j0 = 0; j0 < n; j0 += 64) {
-                    const uint32_t q = b + j0 + lane;
-                    T[j0 + lane < n ? tb + (q >> lg) * sl + (q & bm) * so : kPad] = (uint8_t)v;
-                }
+            const bool run = k < lim && len[k] > 1;
+            rl = run ? len[k] : rl;
+            rq = run ? base + c[k] - len[k] : rq;
+            rv = run ? val[k] : rv;
+        }
+        if (ballot(rl != 0)) {
+            const uint32_t rin = wave_sum_incl(rl), rs = rin - rl, rt = readlane(rin, 63);
+            const uint32_t key = (rq - rs) << 8 | rv;
+            uint32_t carry = 0;  // the run covering the previous chunk's last byte
+            for (uint32_t j0 = 0; j0 < rt; j0 += 64) {
+                Mk[lane] = lane ? 0u : carry;
+                const uint32_t o = rs - j0;
+                Mk[rl != 0 && o < 64 ? o : 64 + lane] = key;
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t kk = wave_scan(Mk[lane], 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+                __builtin_amdgcn_wave_barrier();
+                carry = readlane(kk, 63);
+                const uint32_t q = j0 + lane + (kk >> 8);
+                T[j0 + lane < rt ? at(q) : kPad] = (uint8_t)kk;
             }
         }
         if (hit) {
@@ -3240,10 +3265,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_UNB_WPE)
 {
     __shared__ uint8_t T[kTile * kDS];
     __shared__ uint32_t ring[4][256];
+    __shared__ uint32_t marks[4][128];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t ntiles = ws.ctr[2];
     RevChain ca;
     ca.rd.R = reinterpret_cast<uint8_t *>(ring[wv]);
+    ca.Mk = marks[wv];
     ca.rd.lane = lane;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t tid = tid_here(), lane = tid & 63, wv = tid >> 6;
