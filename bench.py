@@ -45,7 +45,7 @@ PMC_PATH = os.path.join(ROOT, "profiles", "pmc_summary.json")
 FGK_SRC = os.path.join(ROOT, "huffman-codec_amd", "csrc", "hc_fgk.hip")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -60,7 +60,12 @@ def parse():
                          "(the north star's final gather), timed and reported separately")
     ap.add_argument("--no-configs", action="store_true", help="N=1: skip the other BASELINE configs")
     ap.add_argument("--only-configs", default="", help="comma list: run just these configs (no headline)")
-    return ap.parse_args()
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL on ROCm): the GPU run; gloo: a CPU dry run of the multi-rank path "
+                         "(sharding, barriers, timing, max-over-ranks, counter reduction, --gather) with a "
+                         "stand-in per-rank step that copies each stream instead of coding it")
+    ap.add_argument("--dry-stream-bytes", type=int, default=4096, help="gloo dry run: bytes per stream")
+    return ap.parse_args(argv)
 
 
 def sha(b):
@@ -228,19 +233,38 @@ class Batch:
         return self.enc[o:o + n].cpu().numpy().tobytes()
 
 
+class HostEvent:
+    """torch.cuda.Event's record / elapsed_time on the host clock (the gloo dry run)"""
+
+    def __init__(self, **_):
+        self.t = None
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+def sync(torch, dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def timed(torch, b, stream, steps, warmup, barrier=None):
     """warmup + `steps` timed round trips; returns (wall seconds, enc ms, dec ms per launch)"""
     for _ in range(warmup):
         b.step(stream)
-    torch.cuda.synchronize(b.dev)
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    sync(torch, b.dev)
+    Ev = torch.cuda.Event if b.dev.type == "cuda" else HostEvent
+    events = [[Ev(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     if barrier:
         barrier()
-    torch.cuda.synchronize(b.dev)
+    sync(torch, b.dev)
     t0 = time.perf_counter()
     for k in range(steps):
         b.step(stream, events[k])
-    torch.cuda.synchronize(b.dev)
+    sync(torch, b.dev)
     if barrier:
         barrier()
     t1 = time.perf_counter()
@@ -505,6 +529,53 @@ def copy_peak(torch, dev, stream, nbytes=1 << 30, reps=5):
     return round(2 * nbytes / (best * 1e-3) / 1e9, 1)
 
 
+class StandInBatch:
+    """The gloo dry run's per-rank work: S host streams of N pseudo-random bytes (stream k seeded by
+    its global index k) with the same buffers, offsets and bookkeeping as Batch, whose step COPIES
+    each stream into its encode slot and back instead of coding it. It exercises bench.py's
+    multi-rank path (shards, barriers, timing, reductions, --gather) without a GPU; its numbers
+    measure nothing about the codec."""
+
+    def __init__(self, torch, k0, S, N):
+        self.torch, self.dev, self.S, self.N = torch, torch.device("cpu"), S, N
+        self.cap = N + 64
+        self.raw = torch.cat([stand_in_stream(torch, k, N) for k in range(k0, k0 + S)]) if S else \
+            torch.empty(0, dtype=torch.uint8)
+        i64 = dict(dtype=torch.int64)
+        self.offs = torch.arange(S, **i64) * N
+        self.lens = torch.full((S,), N, **i64)
+        self.enc = torch.zeros(S * self.cap, dtype=torch.uint8)
+        self.eoffs = torch.arange(S, **i64) * self.cap
+        self.elens = torch.zeros(S, **i64)
+        self.back = torch.empty_like(self.raw)
+        self.blens = torch.zeros_like(self.lens)
+
+    def step(self, stream, ev=None):
+        encv = self.enc.view(self.S, self.cap)
+        if ev is not None:
+            ev[0].record(stream)
+        encv[:, :self.N] = self.raw.view(self.S, self.N)
+        self.elens.fill_(self.N)
+        if ev is not None:
+            ev[1].record(stream)
+        self.back.view(self.S, self.N)[:] = encv[:, :self.N]
+        self.blens.copy_(self.elens)
+        if ev is not None:
+            ev[2].record(stream)
+
+    def bad(self):
+        return int((self.blens != self.lens).sum()) + (0 if self.torch.equal(self.back, self.raw) else 1)
+
+    def fgk_symbols(self):
+        return 0
+
+
+def stand_in_stream(torch, k, N):
+    """stream k of the gloo dry run: N bytes from a generator seeded with k"""
+    g = torch.Generator().manual_seed(0x5EED + k)
+    return torch.randint(0, 256, (N,), generator=g, dtype=torch.int64).to(torch.uint8)
+
+
 def time_gather(torch, hcdist, b, dev, barrier):
     """every rank's encoded streams packed back to back on its GPU (hc_pack_batch), then sent to
     rank 0 point to point; max over ranks of the wall time; rank 0 checks the bytes it got"""
@@ -512,17 +583,20 @@ def time_gather(torch, hcdist, b, dev, barrier):
     for _ in range(2):
         if barrier:
             barrier()
-        torch.cuda.synchronize(dev)
+        sync(torch, dev)
         t0 = time.perf_counter()
         packed, sizes = hcdist.gather_encoded(b.enc, b.eoffs, b.elens)
-        torch.cuda.synchronize(dev)
+        sync(torch, dev)
         if barrier:
             barrier()
         ms.append((time.perf_counter() - t0) * 1e3)
     ms = float(hcdist.reduce_counters([min(ms)], op="max", device=dev)[0])
     total = int(sizes.sum())
     out = {"bytes_to_rank0": total, "ms": round(ms, 3), "GBps": round(total / (ms * 1e-3) / 1e9, 2),
-           "how": "hc_pack_batch on each GPU, then batch_isend_irecv to rank 0 (RCCL p2p over xGMI)"}
+           "how": "hc_pack_batch on each GPU, then batch_isend_irecv to rank 0 (RCCL p2p over xGMI)"
+           if dev.type == "cuda" else "host packing, then batch_isend_irecv to rank 0 (gloo dry run)"}
+    if packed is not None:
+        out["packed_sha256"] = sha(packed.cpu().numpy().tobytes())
     if packed is not None:
         k = b.S - 1  # rank 0's own last stream sits at the end of its shard in the packed buffer
         at = int(b.elens[:k].sum())
@@ -531,8 +605,8 @@ def time_gather(torch, hcdist, b, dev, barrier):
     return out
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
     import torch
     import torch.distributed as dist
     import hcdist
@@ -541,15 +615,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    if not hc.device_ok():
-        raise SystemExit("libhcodec.so: no usable gfx950 device")
-    stream = torch.cuda.current_stream(dev)
+    dry = args.backend == "gloo"  # the CPU dry run of this same path (StandInBatch per rank)
+    if dry:
+        if world > 1:
+            dist.init_process_group("gloo")
+        dev, stream = torch.device("cpu"), None
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+        if not hc.device_ok():
+            raise SystemExit("libhcodec.so: no usable gfx950 device")
+        stream = torch.cuda.current_stream(dev)
 
-    if args.only_configs:
+    if args.only_configs and not dry:
         res, bad = run_configs(torch, hc, dev, stream, set(args.only_configs.split(",")))
         print(json.dumps({"configs": res, "bad": bad}), flush=True)
         raise SystemExit(1 if bad else 0)
@@ -558,7 +638,8 @@ def main():
         raise SystemExit(f"--streams {args.streams} does not split over {world} ranks")
     S = args.streams // world
     use_diff = not args.no_diff
-    b = Batch(torch, hc, dev, args.kind, rank * S, S, use_diff)
+    N = args.dry_stream_bytes if dry else N_RAW
+    b = StandInBatch(torch, rank * S, S, N) if dry else Batch(torch, hc, dev, args.kind, rank * S, S, use_diff)
     barrier = dist.barrier if world > 1 else None
     wall, enc_ms, dec_ms = timed(torch, b, stream, args.steps, args.warmup, barrier)
 
@@ -571,10 +652,10 @@ def main():
         raise SystemExit(f"bit-exact check FAILED on {bad} items")
 
     step_s = float(elapsed) / args.steps
-    raw_total = world * S * N_RAW
+    raw_total = world * S * N
     value = raw_total / step_s / 2**30
     mode = "cm" if use_diff else "c"
-    roof, issue = roofline(S, N_RAW, enc_bytes, enc_ms, dec_ms, mode, args.kind)
+    roof, issue = (None, None) if dry else roofline(S, N, enc_bytes, enc_ms, dec_ms, mode, args.kind)
     result = {
         "metric": METRIC, "value": round(value, 4), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
@@ -582,21 +663,26 @@ def main():
         "data": f"synthetic {args.kind} (SURVEY.md App. D, seed 0x5EED), generated in HBM",
         "config": {"workload": f"C5: {args.streams} x 512x512 {args.kind} streams over {world} GPU(s) "
                                f"({S} per GPU), {'-c -m' if use_diff else '-c'} encode + decode round trip",
-                   "streams_total": args.streams, "streams_per_gpu": S, "stream_bytes": N_RAW,
+                   "streams_total": args.streams, "streams_per_gpu": S, "stream_bytes": N,
                    "mode": "-c -m" if use_diff else "-c",
                    "parallelism": f"dp{world} (stream shards, no data-path collective)"},
         "roofline": roof, "issue": issue,
         "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
-        "encode_GiBps": round(world * S * N_RAW / (enc_ms * 1e-3) / 2**30, 4),
-        "decode_GiBps": round(world * S * N_RAW / (dec_ms * 1e-3) / 2**30, 4),
+        "encode_GiBps": round(world * S * N / (enc_ms * 1e-3) / 2**30, 4) if enc_ms > 0 else None,
+        "decode_GiBps": round(world * S * N / (dec_ms * 1e-3) / 2**30, 4) if dec_ms > 0 else None,
         "bits_per_byte": round(enc_total * 8 / raw_total, 4), "bit_exact": True,
         "fgk_symbols_per_stream": round(b.fgk_symbols() / S, 1),
     }
-    if world == 1:
+    if dry:
+        result.update({"metric": METRIC + " [gloo dry run: streams copied, not coded]", "dry_run": True,
+                       "backend": "gloo", "bit_exact": None, "fgk_symbols_per_stream": None,
+                       "data": "stand-in: pseudo-random bytes per stream (torch generator seeded by the stream index)"})
+        result["config"]["workload"] = f"dry run: {args.streams} x {N}-byte streams over {world} rank(s) ({S} per rank)"
+    if world == 1 and not dry:
         roof["measured_copy_GBps"] = copy_peak(torch, dev, stream)
     if args.gather:
         result["gather"] = time_gather(torch, hcdist, b, dev, barrier)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not dry:
         host = host_cpus()
         cores = host["usable"]
         sample = min(args.cpu_sample or 8 * cores, S)
@@ -614,17 +700,19 @@ def main():
             result["cpu_baseline"] = cb
             result["bit_exact_vs_reference_streams"] = sample
     del b
-    torch.cuda.empty_cache()
     cbad = 0
-    if world == 1 and not args.no_configs:
-        result["configs"], cbad = run_configs(torch, hc, dev, stream, set())
-        result["configs_bit_exact"] = cbad == 0
+    if not dry:
+        torch.cuda.empty_cache()
+        if world == 1 and not args.no_configs:
+            result["configs"], cbad = run_configs(torch, hc, dev, stream, set())
+            result["configs_bit_exact"] = cbad == 0
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
     if cbad:
         raise SystemExit(f"config checks FAILED on {cbad} items")
+    return result
 
 
 if __name__ == "__main__":

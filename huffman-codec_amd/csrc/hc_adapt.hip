@@ -1740,6 +1740,10 @@ constexpr uint64_t kParMin = 1ull << 20;  // block symbols from which a stream t
 // streams (all of the serial pass's edge cases through the parallel one)
 __device__ uint64_t g_par_min = kParMin;
 __device__ __forceinline__ uint64_t par_min() { return g_par_min; }
+// hc_debug_set_par_skew: par_walk enters every odd chunk this many output bytes off its predicted
+// entry (mod W H), so tests exercise par_fix's re-runs and its repair of the starts[] entries a
+// wrong walk wrote
+__device__ uint64_t g_par_skew = 0;
 #else
 __device__ __forceinline__ uint64_t par_min() { return kParMin; }
 #endif
@@ -1759,6 +1763,9 @@ struct PChk {
     uint64_t o_q;       // the process at the chunk start (offset, state; r_q 0xFF: not reached)
     uint32_t r_q, r_out;
     uint64_t o_out;     // ... and at its end
+    uint64_t e_lo, e_hi;  // par_walk: the lowest and highest start entries it wrote (e_lo > e_hi:
+                          // none); a walk from a wrong entry numbers its blocks wrongly, and par_fix
+                          // rewrites every entry in such a range from the exact process
 };
 
 // parallel block-boundary pass (bounds_par below): the data a stream of `cap` symbols reserves
@@ -1771,9 +1778,11 @@ __device__ inline uint64_t par_bytes(uint64_t cap)
            2 * align_up(4ull * kZcap * ns, 16) + align_up(kSub / 4 * ns, 16);
 }
 
-// u64 block-start entries per stream (W H <= cap, W, H >= 8): mode 0 ceil(H/B) ceil(W/128) <=
-// (H/8 + 1)(W/128 + 1) <= WH/1024 + WH/64 + WH/1024 + 1; mode 1 far fewer; mode 2
-// <= 4 W H / 1024 + 1 (dec_header_kernel)
+// u64 block-start entries per stream (W H <= cap, W, H >= 8). Mode 0 records every block:
+// ceil(W/B) ceil(H/B) <= (W + 7)(H + 7) / 64 for B >= 8, and (W + 7)(H + 7) / 64 <= WH / 32 + 16
+// <=> 7W + 7H + 49 <= WH + 1024 <=> 0 <= (W - 7)(H - 7) + 975, true for W, H >= 8; mode 1 far
+// fewer; mode 2 <= 4 W H / 1024 + 1; forged headers that would need more take larger groups
+// (dec_header_kernel)
 __device__ __forceinline__ uint64_t group_entries_bound(uint64_t cap) { return cap / 32 + 16; }
 
 // symbols the FGK stage may write: the count, unless the payload cannot hold it (the first symbol
@@ -1913,7 +1922,7 @@ __global__ __launch_bounds__(1024) void dec_header_kernel(DecArgs a, Ws ws)
         m.ents = m.mode == 0 ? nb : m.groups;
         m.chunks = m.diff ? cdiv(w * h, kChunk) : 0;
         // many block symbols: the parallel boundary pass (the slab holds its data, dec_plan)
-        m.par = m.pcap && nb && count - m.hdr >= par_min();
+        m.par = m.pcap && nb && count > m.hdr && count - m.hdr >= par_min();
         m.nsub = m.par ? cdiv(count - m.hdr, kSub) : 0;
         m.nchk = cdiv(m.nsub, kSubPerChunk);
         m.pfall = 0;
@@ -2054,6 +2063,7 @@ struct BWalk {
     uint64_t pos, blk, got, want;
     uint64_t bx, by, kq, gq;  // block column / row; blk mod K, blk / K (K = 1 in mode 0: every block)
     uint32_t r, last;
+    uint64_t e_lo, e_hi;  // the lowest and highest entries written (e_lo > e_hi: none)
 
     __device__ void init(const AMeta &M, const uint8_t *sym, uint64_t *st, uint32_t l)
     {
@@ -2069,6 +2079,15 @@ struct BWalk {
         per_row = cdiv(W, B);
         nb = per_row * cdiv(H, B);
         lane = l;
+        e_lo = ~0ull;
+        e_hi = 0;
+    }
+    // starts[e] := q (lane 0 stores; every lane tracks the range)
+    __device__ __forceinline__ void record(uint64_t e, uint64_t q)
+    {
+        if (lane == 0) starts[e] = q;
+        e_lo = e < e_lo ? e : e_lo;
+        e_hi = e > e_hi ? e : e_hi;
     }
     __device__ Geo geo() const
     {
@@ -2121,7 +2140,7 @@ struct BWalk {
         gq = blk / K;
         if (got == 0) {
             r = 0;
-            if (kq == 0 && q >= rec_from && lane == 0 && entry() < ents) starts[entry()] = q;
+            if (kq == 0 && q >= rec_from && entry() < ents) record(entry(), q);
         }
     }
     __device__ void load(uint64_t p, uint32_t *w) const
@@ -2207,7 +2226,7 @@ struct BWalk {
                 lo = j + 1;
                 ++blk;
                 const uint64_t e = next_block();
-                if (blk < nb && lane == 0 && e < ents && pos + lo >= rec_from) starts[e] = pos + lo;
+                if (blk < nb && e < ents && pos + lo >= rec_from) record(e, pos + lo);
                 // the next block starts in state 0 (the previous symbol does not matter then; at a
                 // chunk exit on a block end the state is not compared either: par_fix)
                 r = 0;
@@ -2954,12 +2973,20 @@ __global__ __launch_bounds__(256) void par_walk_kernel(DecArgs a, Ws ws)
         w.init(M, at<uint8_t>(ws, M.sym), at<uint64_t>(ws, M.starts), lane);
         const uint64_t q0 = C.q0;
         if (q0 > q || q0 < M.hdr || C.r_in > 3) {  // no prediction: par_fix runs the chunk
-            if (lane == 0) C.r_q = 0xFFu;
+            if (lane == 0) {
+                C.r_q = 0xFFu;
+                C.e_lo = ~0ull;
+                C.e_hi = 0;
+            }
             continue;
         }
-        w.enter(q0, C.r_in, C.o_in, q);
+        uint64_t o_in = C.o_in;
+#ifdef HC_DEBUG_HOOKS
+        if (g_par_skew && (j / kSubPerChunk) % 2 == 1) o_in = (o_in + g_par_skew) % (M.w * M.h);
+#endif
+        w.enter(q0, C.r_in, o_in, q);
         uint32_t r_q = C.r_in;
-        uint64_t o_q = C.o_in;
+        uint64_t o_q = o_in;
         int st = 0;
         if (q0 < q) {  // run in from the window's block start (recording nothing before q)
             st = w.run(q, q);
@@ -2973,6 +3000,8 @@ __global__ __launch_bounds__(256) void par_walk_kernel(DecArgs a, Ws ws)
             C.st = (uint32_t)st;
             C.r_out = w.r;
             C.o_out = w.offset();
+            C.e_lo = w.e_lo;
+            C.e_hi = w.e_hi;
         }
     }
 }
@@ -2980,14 +3009,20 @@ __global__ __launch_bounds__(256) void par_walk_kernel(DecArgs a, Ws ws)
 // one wave per stream: chunk entries against the exact exits before them, 64 chunks at a time
 // (lane k: chunk c, its predicted entry against chunk c - 1's exit); the first chunk that differs
 // (or every chunk, after a fallback) is re-run here from the exact exit, then the check goes on
-// after it; the first error in chunk order is the stream's status
+// after it; the first error in chunk order is the stream's status.
+// A walk from a wrong entry numbers its blocks wrongly, so the entries it wrote (its e_lo..e_hi)
+// may belong to blocks of other chunks, whose own walks raced with it. The re-run rewrites only
+// the re-run chunk's blocks; afterwards every chunk whose blocks meet such a range is walked once
+// more from its exact entry (kept in C by the first pass), which rewrites each entry there with
+// its true start (tests/bounds_par_model.py keeps a walk's starts aside until it is verified; the
+// GPU pass writes them at once and repairs them here).
 __global__ __launch_bounds__(64) void par_fix_kernel(DecArgs a, Ws ws)
 {
     const uint32_t lane = lane_id();
     for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
         AMeta &M = ws.meta[i];
         if (M.status || !M.par) continue;
-        const PChk *C = pchk(ws, M);
+        PChk *C = pchk(ws, M);
         BWalk w;
         w.init(M, at<uint8_t>(ws, M.sym), at<uint64_t>(ws, M.starts), lane);
         const Geo g = w.geo();
@@ -2995,6 +3030,8 @@ __global__ __launch_bounds__(64) void par_fix_kernel(DecArgs a, Ws ws)
         const uint64_t nchk = M.nchk, span = (uint64_t)kSub * kSubPerChunk;
         uint32_t r = 0, st = 0;  // the exact process before chunk c
         uint64_t o = 0, reruns = 0, c = 0;
+        uint64_t dlo = ~0ull, dhi = 0;  // entries written by walks from wrong entries
+        if (nchk == 0) st = HC_ERR_BLOCK_EOF;  // blocks and no block symbols (transform.cpp:170-174)
         while (c < nchk && !st) {
             const uint64_t cl = c + lane;
             const bool on = cl < nchk;
@@ -3024,12 +3061,49 @@ __global__ __launch_bounds__(64) void par_fix_kernel(DecArgs a, Ws ws)
                 break;
             }
             ++reruns;  // re-run chunk c from the exact process
+            if (!fall && C[c].r_q != 0xFFu && C[c].e_lo <= C[c].e_hi) {
+                dlo = min(dlo, C[c].e_lo);
+                dhi = max(dhi, C[c].e_hi);
+            }
             const uint64_t q = M.hdr + c * span, qe = q + span < M.count ? q + span : M.count;
             w.enter(q, r, o, q);
             st = (uint32_t)w.run(qe, q);
+            // the exact entry and exit, for the repair pass
+            if (lane == 0) {
+                C[c].r_q = r;
+                C[c].o_q = o;
+                C[c].r_out = w.r;
+                C[c].o_out = w.offset();
+                C[c].st = st;
+            }
             r = w.r;
             o = w.offset();
             ++c;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // lane 0's C[] writes, read back below
+        // repair: walk again every chunk whose blocks (those that start between its exact entry
+        // and exit offsets) meet the entries a wrong walk wrote
+        if (st == 0 && dlo <= dhi) {
+            for (uint64_t c0 = 0; c0 < nchk; c0 += 64) {
+                const uint64_t cl = c0 + lane;
+                bool hit = false;
+                if (cl < nchk) {
+                    auto ent = [&](uint64_t off) -> uint64_t {
+                        if (off >= g.total) return g.nb / M.K;
+                        uint64_t bx, by, rel;
+                        g.locate(off, bx, by, rel);
+                        return (by * g.per_row + bx) / M.K;
+                    };
+                    const uint64_t lo = ent(C[cl].o_q), hi = ent(C[cl].o_out);
+                    hit = lo <= dhi && hi >= dlo;
+                }
+                for (uint64_t hm = ballot(hit); hm; hm &= hm - 1) {
+                    const uint64_t cc = c0 + (uint64_t)__builtin_ctzll(hm);
+                    const uint64_t q = M.hdr + cc * span, qe = q + span < M.count ? q + span : M.count;
+                    w.enter(q, C[cc].r_q, C[cc].o_q, q);
+                    (void)w.run(qe, q);
+                }
+            }
         }
         if (lane == 0) {
             M.status = (int32_t)st;
@@ -3585,7 +3659,7 @@ uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t
     // symbols <= 8 per payload byte (+64 slack); u64 block starts <= 8 (out_cap / 32 + 16) (see
     // group_entries_bound); chunk sums out_cap / 16384
     // + the parallel boundary pass: per symbol of the streams that take it, the Z entries and
-    // their window info (8 kZcap / kSub bytes: 2 at kZcap 512), packed s0 0.25, records; 4672
+    // their window info (8 kZcap / kSub bytes: 4 at kZcap 1024), packed s0 0.25, records; 4992
     // bytes of rounding per stream
     constexpr uint64_t kPar8 = (8 * (8 * kZcap + kSub / 4 + 64) + kSub - 1) / kSub;  // per 8 symbols
     return ws_header(n) + (8 + kPar8) * total_in + total_out / 4 + total_out / kChunk + 4992ull * n + 4096;
@@ -3720,6 +3794,12 @@ hipError_t adapt_decode_batch(const Batch &b, void *work, uint64_t work_bytes, h
 }  // namespace hc
 
 #ifdef HC_DEBUG_HOOKS
+extern "C" int hc_debug_set_par_skew(uint64_t bytes)
+{
+    // 0: off; else every odd chunk of the parallel boundary pass walks from a wrong entry
+    return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_par_skew), &bytes, sizeof(bytes)) == hipSuccess ? 0 : HC_ERR_DEVICE;
+}
+
 extern "C" int hc_debug_set_par_min(uint64_t symbols)
 {
     // block symbols from which an adaptive stream's boundaries take the parallel pass

@@ -44,6 +44,10 @@ struct DevBuf {
     void give_back()
     {
         if (!p) return;
+        // the single-buffer API runs on the null stream; a call that returns early (an error
+        // after an asynchronous launch) may still have kernels writing this buffer, so wait for
+        // them before the next call can take it
+        (void)hipStreamSynchronize(nullptr);
         FreeList &f = free_list();
         {
             std::lock_guard<std::mutex> lk(f.mu);
@@ -322,6 +326,15 @@ int hc_compress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t
                       uint32_t n_streams, uint32_t flags, uint8_t *out, const uint64_t *out_offs,
                       const uint64_t *out_caps, uint64_t *out_lens, int32_t *status, void *stream)
 {
+    return hc_compress_batch_aux(in, in_offs, in_lens, n_streams, flags, out, out_offs, out_caps, out_lens, status,
+                                 stream, nullptr);
+}
+
+int hc_compress_batch_aux(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                          uint32_t n_streams, uint32_t flags, uint8_t *out, const uint64_t *out_offs,
+                          const uint64_t *out_caps, uint64_t *out_lens, int32_t *status, void *stream,
+                          void *aux_stream)
+{
     if (n_streams == 0) return HC_OK;
     if (!in || !in_offs || !in_lens || !out || !out_offs || !out_caps || !out_lens || !status)
         return HC_ERR_ARG;
@@ -329,7 +342,7 @@ int hc_compress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t
     if (!aligned4(in) || !aligned4(out)) return HC_ERR_ARG;
     Batch b{in, in_offs, in_lens, n_streams, out, out_offs, out_caps, out_lens, status, flags};
     const hipError_t e = hc::launch_encode(b, (flags & HC_FLAG_DIFF) ? hc::SRC_RAW_DIFF : hc::SRC_RAW,
-                                           static_cast<hipStream_t>(stream));
+                                           static_cast<hipStream_t>(stream), static_cast<hipStream_t>(aux_stream));
     return e == hipSuccess ? HC_OK : HC_ERR_DEVICE;
 }
 

@@ -23,7 +23,6 @@
 //    descriptors whose hardware range check replaces per-lane bounds tests.
 //  * Output bits gather in a 64-bit scalar accumulator, flush as big-endian dwords into a VGPR
 //    stage and leave as one coalesced 256-byte buffer store per 64 words.
-#include <mutex>
 #include <type_traits>
 
 #include "hc_internal.h"
@@ -1796,49 +1795,33 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
 // streams that the table-mode encoder holds resident at once: 6 waves per SIMD (its LDS)
 static uint32_t table_slots()
 {
-    static uint32_t slots = 0;
-    if (!slots) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        slots = (uint32_t)cus * 24;
-    }
-    return slots;
-}
-
-// A second stream per device for the table-mode launches, so that they run beside the cache-mode
-// launches (never destroyed: the HIP runtime may be gone at exit; concurrent calls may share it,
-// each joins only its own work through its own events)
-static hipStream_t aux_stream()
-{
-    static std::mutex mu;
-    static hipStream_t aux[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!aux[dev] && hipStreamCreateWithFlags(&aux[dev], hipStreamNonBlocking) != hipSuccess) aux[dev] = nullptr;
-    return aux[dev];
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    return (uint32_t)cus * 24;
 }
 
 template <int kSrc>
-static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipStream_t st)
+static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipStream_t st, hipStream_t aux)
 {
     // every stream votes for its mode (enc_mode_kernel); the cache-mode launches run on the
-    // caller's stream and the table-mode launches beside them on the aux stream, each skipping
-    // the other mode's streams (so a mixed batch fills the GPU with both at once)
+    // caller's stream, each skipping the other mode's streams. The table-mode launches follow them
+    // on the same stream, or -- when the caller gives a second stream -- run beside them there
+    // (forked and joined by events), so that a mixed batch fills the GPU with both at once. The
+    // library keeps no stream of its own.
     enc_mode_kernel<kSrc><<<(b.n + 3) / 4, 256, 0, st>>>(b, b.n <= table_slots() ? 1u : 0u, enc_tab());
-    hipStream_t aux = aux_stream();
     hipEvent_t fork = nullptr, join = nullptr;
+    if (aux == st) aux = nullptr;
     if (aux && (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess))
         aux = nullptr;
     hipStream_t ts = st;  // the table-mode launches' stream
     if (aux && hipEventRecord(fork, st) == hipSuccess && hipStreamWaitEvent(aux, fork, 0) == hipSuccess) ts = aux;
     encode_kernel<0, kSrc><<<grid, block, 0, st>>>(b);
-    encode_kernel<0, kSrc, true><<<grid, block, 0, ts>>>(b);
     encode_kernel<1, kSrc><<<grid, block, 0, st>>>(b);
-    encode_kernel<1, kSrc, true><<<grid, block, 0, ts>>>(b);
     encode_kernel<2, kSrc><<<grid, block, 0, st>>>(b);
+    encode_kernel<0, kSrc, true><<<grid, block, 0, ts>>>(b);
+    encode_kernel<1, kSrc, true><<<grid, block, 0, ts>>>(b);
     hipError_t e = hipGetLastError();
     if (ts != st) {
         const hipError_t e1 = hipEventRecord(join, ts);
@@ -1850,7 +1833,7 @@ static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipSt
     return e;
 }
 
-hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st)
+hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st, hipStream_t aux)
 {
     if (b0.n == 0) return hipSuccess;
     Batch b = b0;
@@ -1859,9 +1842,9 @@ hipError_t launch_encode(const Batch &b0, EncSrc src, hipStream_t st)
     // enc_mode_kernel marks each stream for the cache or the table launch; then one launch per
     // tree layout and mode, each stream coded by exactly one of them (tree_kind, the mark)
     switch (src) {
-    case SRC_RAW: return launch_encode_src<SRC_RAW>(b, grid, block, st);
-    case SRC_RAW_DIFF: return launch_encode_src<SRC_RAW_DIFF>(b, grid, block, st);
-    default: return launch_encode_src<SRC_SYMBOLS>(b, grid, block, st);
+    case SRC_RAW: return launch_encode_src<SRC_RAW>(b, grid, block, st, aux);
+    case SRC_RAW_DIFF: return launch_encode_src<SRC_RAW_DIFF>(b, grid, block, st, aux);
+    default: return launch_encode_src<SRC_SYMBOLS>(b, grid, block, st, aux);
     }
 }
 

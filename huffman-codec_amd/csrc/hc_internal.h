@@ -32,7 +32,7 @@ constexpr uint64_t kNarrowMaxSymbols = (1ull << 22) - 2;
 constexpr uint64_t kWideMaxSymbols = 0xFFFFFFFFull - 1;
 
 // fused [diff] -> RLE -> FGK encode, or FGK over a ready symbol stream (adaptive path)
-hipError_t launch_encode(const Batch &b, EncSrc src, hipStream_t st);
+hipError_t launch_encode(const Batch &b, EncSrc src, hipStream_t st, hipStream_t aux = nullptr);
 // fused FGK decode -> RLE revert -> [diff revert] (diff taken from each stream's flags byte),
 // or FGK decode to the symbol stream
 hipError_t launch_decode(const Batch &b, DecDst dst, hipStream_t st);

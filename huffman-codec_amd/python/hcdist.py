@@ -13,7 +13,9 @@ import torch.distributed as dist
 
 
 def shard(rank, world, per_rank):
-    """Global stream indices owned by `rank` (weak scaling: per_rank streams each)."""
+    """Global stream indices owned by `rank`: the contiguous range [rank * per_rank, (rank + 1) * per_rank).
+    bench.py splits a fixed total over the ranks (strong scaling: per_rank = total / world); a
+    caller that fixes per_rank instead scales weakly."""
     return range(rank * per_rank, (rank + 1) * per_rank)
 
 

@@ -95,6 +95,8 @@ def _load(path):
     L.hc_free.argtypes = [vp]
     L.hc_compress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
                                     vp, vp]
+    L.hc_compress_batch_aux.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
+                                        vp, vp, vp]
     L.hc_decompress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
     L.hc_compress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp]
     L.hc_decompress_host_batch.argtypes = [vp, vp, ctypes.c_uint32, vp, vp, vp, vp]
@@ -196,13 +198,28 @@ def _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, statu
     return n
 
 
+_AUX = {}  # device index -> a side stream for the encoder's table-mode launches (Python-side)
+
+
+def _aux_stream(inp):
+    import torch
+    d = inp.device.index if inp.device.index is not None else torch.cuda.current_device()
+    if d not in _AUX:
+        _AUX[d] = torch.cuda.Stream(device=d)
+    return _AUX[d]
+
+
 def compress_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status,
-                   use_diff=False, stream=None):
-    """hc_compress_batch on torch CUDA tensors (uint8 data, int64 offsets/lengths, int32 status)."""
+                   use_diff=False, stream=None, aux_stream="auto"):
+    """hc_compress_batch_aux on torch CUDA tensors (uint8 data, int64 offsets/lengths, int32
+    status). aux_stream: a second stream for the table-mode launches ("auto": one side stream
+    per device kept by this module; None: both modes one after the other on `stream`)."""
     n = _check_batch(inp, in_offs, in_lens, out, out_offs, out_caps, out_lens, status)
-    rc = lib().hc_compress_batch(_dp(inp), _dp(in_offs), _dp(in_lens), n,
-                                 HC_FLAG_DIFF if use_diff else 0, _dp(out), _dp(out_offs),
-                                 _dp(out_caps), _dp(out_lens), _dp(status), _stream_handle(stream))
+    aux = _aux_stream(inp) if aux_stream == "auto" else aux_stream
+    rc = lib().hc_compress_batch_aux(_dp(inp), _dp(in_offs), _dp(in_lens), n,
+                                     HC_FLAG_DIFF if use_diff else 0, _dp(out), _dp(out_offs),
+                                     _dp(out_caps), _dp(out_lens), _dp(status), _stream_handle(stream),
+                                     ctypes.c_void_p(None) if aux is None else _stream_handle(aux))
     if rc:
         raise HCodecError(f"hc_compress_batch failed: {rc}")
 
@@ -379,6 +396,17 @@ def debug_set_par_min(symbols):
     rc = f(int(symbols))
     if rc:
         raise HCodecError(f"hc_debug_set_par_min failed: {rc}")
+
+
+def debug_set_par_skew(nbytes):
+    """Test hook (debug build only, use_debug_build): every odd chunk of the parallel block-boundary
+    pass walks from its predicted entry shifted by `nbytes` output bytes (0: off), forcing par_fix's
+    re-runs and its repair of the block starts a wrong walk wrote."""
+    f = _dbg().hc_debug_set_par_skew
+    f.argtypes = [ctypes.c_uint64]
+    rc = f(int(nbytes))
+    if rc:
+        raise HCodecError(f"hc_debug_set_par_skew failed: {rc}")
 
 
 def debug_stage_clock(on):

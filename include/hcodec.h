@@ -90,6 +90,18 @@ int hc_compress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t
                       const uint64_t *out_caps, uint64_t *out_lens, int32_t *status,
                       void *stream);
 
+/* The same, with a second caller-owned HIP stream (or NULL) for the encoder's table-mode
+ * launches. Each stream is coded in one of two modes, voted per stream from its alphabet: the
+ * path cache (skewed alphabets) or the level tables (flat ones); the two modes are separate
+ * launches. With aux_stream they run side by side (forked from and joined back into `stream` by
+ * events, also under graph capture), so a batch mixing both kinds fills the GPU with both at once;
+ * hc_compress_batch (aux_stream NULL) runs them one after the other on `stream`. The library
+ * keeps no stream of its own. */
+int hc_compress_batch_aux(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
+                          uint32_t n_streams, uint32_t flags, uint8_t *out, const uint64_t *out_offs,
+                          const uint64_t *out_caps, uint64_t *out_lens, int32_t *status, void *stream,
+                          void *aux_stream);
+
 /* Decompress n_streams encoded streams (non-adaptive: a stream whose flags byte has bit 6 set
  * gets HC_ERR_UNSUPPORTED here; use hc_decompress_adapt_batch). FGK -> RLE revert -> [diff revert], fused. */
 int hc_decompress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,

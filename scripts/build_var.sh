@@ -1,10 +1,10 @@
 #!/bin/bash
-# Build a variant of libhcodec_dbg.so with extra compiler flags into build_ab/<name>/:
+# Build a variant of libhcodec_dbg.so with extra compiler flags into abvar/<name>/:
 #   bash scripts/build_var.sh <name> [flags...]      e.g. build_var.sh nostore -DHC_EXP_NOSTORE
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-out=build_ab/$name
+out=abvar/$name
 mkdir -p "$out/obj"
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -Ihuffman-codec_amd/csrc -Wall -Wno-pass-failed -mllvm -structurizecfg-skip-uniform-regions=1 -DHC_DEBUG_HOOKS"
 pids=()

@@ -1,10 +1,10 @@
 #!/bin/bash
-# A/B of whole-library variants (build_ab/<v>/libhcodec_dbg.so) on bench configs:
+# A/B of whole-library variants (abvar/<v>/libhcodec_dbg.so) on bench configs:
 #   CONFIGS=C3,noise bash scripts/cfg_ab.sh base variant ...
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for r in 1 2; do
 for v in "$@"; do
-  HC_LIB_PATH=build_ab/$v/libhcodec_dbg.so HC_DBG_LIB_PATH=build_ab/$v/libhcodec_dbg.so timeout -k 10 400 \
+  HC_LIB_PATH=abvar/$v/libhcodec_dbg.so HC_DBG_LIB_PATH=abvar/$v/libhcodec_dbg.so timeout -k 10 400 \
     python3 -u bench.py --only-configs ${CONFIGS:-C3} > gpurun_out/cfg_ab_$v.log 2>&1 || exit $?
   python3 - "$v" <<'PY'
 import json, sys

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 (second session): A/B of the adaptive tile kernels (build_ab/<dirs>), then the full
+# Round-3 (second session): A/B of the adaptive tile kernels (abvar/<dirs>), then the full
 # GPU check (parity tests + bench). Every GPU step has its own limit; a crash ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

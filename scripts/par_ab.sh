@@ -1,8 +1,8 @@
 #!/bin/bash
-# A/B of parallel-pass variants (build_ab/<v>/libhcodec_dbg.so) on C4 / C4m: bench stages
+# A/B of parallel-pass variants (abvar/<v>/libhcodec_dbg.so) on C4 / C4m: bench stages
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for v in "$@"; do
-  HC_LIB_PATH=build_ab/$v/libhcodec_dbg.so HC_DBG_LIB_PATH=build_ab/$v/libhcodec_dbg.so timeout -k 10 300 \
+  HC_LIB_PATH=abvar/$v/libhcodec_dbg.so HC_DBG_LIB_PATH=abvar/$v/libhcodec_dbg.so timeout -k 10 300 \
     python3 -u bench.py --only-configs C4,C4m > gpurun_out/par_ab_$v.log 2>&1 || exit $?
   python3 - "$v" <<'PY'
 import json, sys

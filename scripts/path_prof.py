@@ -5,8 +5,8 @@ s_memtime cycles of each region into lane i of an accumulator and stores lanes 0
 g_trace[8 * stream + i] (lane 0 = the wave's whole life). s_memtime itself costs cycles, so
 the shares are indicative, not exact.
 
-    make -C huffman-codec_amd lib/libhcodec.so EXTRA=-DHC_PROF -B && cp ... build_ab/P/
-    HC_LIB_PATH=build_ab/P/libhcodec.so python scripts/path_prof.py [--streams 8192]
+    make -C huffman-codec_amd lib/libhcodec.so EXTRA=-DHC_PROF -B && cp ... abvar/P/
+    HC_LIB_PATH=abvar/P/libhcodec.so python scripts/path_prof.py [--streams 8192]
 """
 import argparse
 import ctypes

@@ -1,6 +1,6 @@
 """Phase shares of tile_cost_kernel (diagnostic; needs a -DHC_TC_PROF build via HC_LIB_PATH).
 
-    HC_LIB_PATH=build_ab/TCP/libhcodec.so python scripts/tc_prof.py [--streams 8192]
+    HC_LIB_PATH=abvar/TCP/libhcodec.so python scripts/tc_prof.py [--streams 8192]
 """
 import argparse
 import ctypes

@@ -95,3 +95,38 @@ def test_pack_single_process():
     offs = torch.tensor([0, 10, 30])
     lens = torch.tensor([3, 0, 5])
     assert hcdist.pack(buf, offs, lens).tolist() == [0, 1, 2, 30, 31, 32, 33, 34]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_multi_rank_dry_run(world):
+    """bench.py's own multi-rank path (shards, barriers, max-over-ranks timing, counter reduction,
+    --gather) end to end under the driver's launcher, on CPU: --backend gloo swaps each rank's GPU
+    step for a stand-in that copies its streams. Rank 0 prints exactly one JSON line; the gathered
+    payload is every rank's shard in global stream order."""
+    import hashlib
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    S, N = 2 * world, 3000
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--backend", "gloo", "--gpus", str(world), "--streams", str(S), "--steps", "3", "--warmup", "1",
+           "--gather", "--dry-stream-bytes", str(N)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    r = json.loads(lines[0])
+    assert r["dry_run"] is True and r["n_gpus"] == world and r["steps"] == 3 and r["warmup"] == 1
+    assert r["config"]["streams_total"] == S and r["config"]["streams_per_gpu"] == 2
+    assert r["value"] > 0 and r["ms_per_step"] > 0 and r["scaling"] == "strong"
+    assert r["bits_per_byte"] == 8.0  # the stand-in copies: encoded = raw bytes
+    sys.path.insert(0, root)
+    import bench
+    want = torch.cat([bench.stand_in_stream(torch, k, N) for k in range(S)]).numpy().tobytes()
+    g = r["gather"]
+    assert g["bytes_to_rank0"] == S * N and g["rank0_spot_check"] is True
+    assert g["packed_sha256"] == hashlib.sha256(want).hexdigest()

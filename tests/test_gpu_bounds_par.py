@@ -126,3 +126,55 @@ def test_par_bounds_real_threshold_constant_runs(gpu, hc, oracle_mod):
         assert gst == wst, (k, gst, wst)
         if wst == 0:
             assert got == want, k
+
+
+@pytest.mark.parametrize("skew", [1, 4099, 777777])
+def test_par_bounds_wrong_entries_repaired(gpu, hc, oracle_mod, skew):
+    """every odd chunk of the parallel pass walks from a wrong entry (hc_debug_set_par_skew): its
+    walk writes block starts under wrong block numbers, racing with the neighbouring chunks' walks.
+    par_fix must re-run those chunks and rewrite the entries they touched: the decoded bytes and
+    statuses still equal the oracle's (valid and damaged streams, threshold 0 and real sizes)."""
+    torch = gpu
+    hc.use_debug_build(True)
+    hc.debug_set_par_min(0)
+    hc.debug_set_par_skew(skew)
+    try:
+        datas, wants, sizes = [], [], []
+        rng = np.random.default_rng(skew)
+        for k, (W, H, use_diff) in enumerate([(2048, 2048, True), (512, 512, False), (512, 512, True),
+                                              (1024, 768, True)]):
+            m = oracle_mod.synth("photo", k, W, H)
+            if use_diff:
+                m = np.frombuffer(oracle_mod.diff(m), dtype=np.uint8)
+            st, stream, _ = oracle_mod.adapt(m, W, H)
+            assert st == 0
+            hdr, x = _adaptive_parts(oracle_mod, stream)
+            for y in [x] + _damaged(rng, x)[:2]:
+                d = B.container(oracle_mod, hdr + y)
+                datas.append(d)
+                wants.append(oracle_mod.decompress(d))
+                sizes.append(W * H)
+        dst, dec, _ = decompress_adapt_batch(hc, torch, datas, sizes)
+        for k, ((wst, want), gst, got) in enumerate(zip(wants, dst, dec)):
+            assert gst == wst, (k, gst, wst)
+            if wst == 0:
+                assert got == want, k
+    finally:
+        hc.debug_set_par_skew(0)
+        hc.debug_set_par_min(1 << 20)
+        hc.use_debug_build(False)
+
+
+def test_par_bounds_no_block_symbols(gpu, hc, oracle_mod, par_everywhere):
+    """blocks announced, no block symbol at all (count == header): the reference exits with 14
+    (transform.cpp:170-174) -- also with the parallel pass's threshold at 0"""
+    torch = gpu
+    W = H = 64
+    b = 8
+    nb = (W // b) * (H // b)
+    hdr = list(W.to_bytes(8, "big") + H.to_bytes(8, "big") + b.to_bytes(8, "big")) + [0xFF] * (nb // 8)
+    datas = [B.container(oracle_mod, hdr), B.container(oracle_mod, hdr + [7])]
+    wants = [oracle_mod.decompress(d) for d in datas]
+    assert wants[0][0] == 14
+    dst, dec, _ = decompress_adapt_batch(hc, torch, datas, [W * H] * len(datas))
+    assert dst == [w[0] for w in wants]
