@@ -56,11 +56,19 @@ __device__ __forceinline__ uint64_t *trace_buf() { return g_trace; }
 __device__ __forceinline__ uint32_t window_bytes() { return __builtin_amdgcn_readfirstlane(g_window); }
 static uint32_t min_tree() { return g_min_tree; }
 static uint32_t enc_tab() { return g_enc_tab; }
+// 1: narrow streams decode two per wavefront (decode2_kernel), 0: one per wavefront (the default,
+// measured faster: DESIGN.md §3); hc_debug_set_dec_pair, tests run both
+static uint32_t g_dec_pair = 0;
+static uint32_t dec_pair() { return g_dec_pair; }
 #else
 __device__ __forceinline__ uint64_t *trace_buf() { return nullptr; }
 __device__ __forceinline__ uint32_t window_bytes() { return 1u << 30; }
 static uint32_t min_tree() { return 0; }
 static uint32_t enc_tab() { return 0; }
+#ifndef HC_DEC_PAIR
+#define HC_DEC_PAIR 0
+#endif
+static uint32_t dec_pair() { return HC_DEC_PAIR; }
 #endif
 // Streams are addressed through buffer descriptors, whose offsets are 32-bit: each stream's input
 // and output are reached through windows that slide forward by whole multiples of 256 bytes
@@ -277,6 +285,12 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x)
     return x;
 }
 
+// lane l gets x of lane l - 1, lane 0 gets fill (a DPP wave shift: no LDS round trip)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x, uint32_t fill)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x138, 0xF, 0xF, false);
+}
+
 // range-checked view of one stream's bytes; the arguments must be wave-uniform
 __device__ __forceinline__ rsrc_t make_rsrc(const uint8_t *p, uint32_t bytes)
 {
@@ -320,15 +334,16 @@ struct Fgk {
     const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
     uint64_t pacc = 0;        // HC_PROF regions inside the tree code
 
-    __device__ Fgk(Tree<kW, kDec, kTab> &t, uint32_t l)
+    __device__ __forceinline__ Fgk(Tree<kW, kDec, kTab> &t, uint32_t l)
         : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), pc_lb(0), pc_lb_ok(0), gen(0), stale(0), from(0),
           pc_lane(&t.pc[0] + (l & 15u) - (kTabs ? 0 : kRow))
     {
         // huffman.cpp:23-31: a lone NYT root
         // narrow: sentinels above every weight word; the encoder's last word (above kMissPos)
-        // is 0 and the decoder's are all ones - 1, see update_fast
+        // is 0, the decoder's all ones - 1 (see update_fast) but its last 0 too: the pair
+        // (kMissPos, kMissPos + 1) fails every leader test (decode_pair's guard lanes)
         for (uint32_t i = lane; i < kWords; i += 64)
-            T.wt[i] = i <= kRoot ? (Wt)0 : (kWide ? ~(Wt)0 : (Wt)(kTabs ? 0xFFFFFFFEu : (i != kWords - 1 ? 0xFFFFFFFFu : 0u)));
+            T.wt[i] = i <= kRoot ? (Wt)0 : (kWide ? ~(Wt)0 : (Wt)(i == kWords - 1 && (kDec || !kTabs) ? 0u : (kTabs ? 0xFFFFFFFEu : 0xFFFFFFFFu)));
         if (lane < 2) T.lvl_root[lane] = kRoot;
         for (uint32_t i = lane; i < 516; i += 64) {
             T.body[i] = i == kRoot ? (kDec ? kNyt | kNotLeaf : kNyt) : 0;
@@ -433,7 +448,7 @@ struct Fgk {
         pc_lb = lane_read(lw, 15);
     }
 
-    __device__ void pc_drop(uint32_t e)
+    __device__ __forceinline__ void pc_drop(uint32_t e)
     {
         pc_forget(e, scr16(), 0);
         *(lane < kSlotDepth + 2 ? &T.pc[e * kRow + lane] : scr16()) = (uint16_t)(lane < kSlotDepth ? 0xFFFFu : 0u);
@@ -470,7 +485,7 @@ struct Fgk {
     // moves the content of a position some walk passes through: those carry the generation.
     // from = 0: all levels, a new generation; otherwise levels from..8 (the entries above reach
     // neither swapped position, so they and the marks they set stand)
-    __device__ void build_levels()
+    __device__ __forceinline__ void build_levels()
     {
         uint32_t j0 = from;
         if (j0 == 0) {
@@ -504,7 +519,7 @@ struct Fgk {
     // depth, so the lowest matching index names it (level 8's entries stay right: a position
     // they stop at is walked on by the descent). Entries of levels >= from may predate a swap
     // earlier in this walk; a match there gives a level >= from - 1, leaving from as it is.
-    __device__ uint32_t table_level(uint32_t s, uint32_t l)
+    __device__ __forceinline__ uint32_t table_level(uint32_t s, uint32_t l)
     {
         for (uint32_t r = 0; r < 4; ++r) {
             const uint32_t i = r * 64 + lane;
@@ -575,7 +590,7 @@ struct Fgk {
 
     // highest position >= from whose weight equals that of word w, when positions
     // from-64..from-1 all had it (the sentinels above the root end the scan)
-    __device__ uint32_t leader_far(uint32_t from, Wt w)
+    __device__ __forceinline__ uint32_t leader_far(uint32_t from, Wt w)
     {
         const Wt lim = kWide ? w : (w | 1023u);
         for (;;) {
@@ -587,7 +602,7 @@ struct Fgk {
 
     // decoder: the position of symbol sym's leaf, 0xFFFFFFFF if it has none (lane-parallel scan
     // of body[]; only a corrupted stream names a known symbol after the NYT code)
-    __device__ uint32_t find_leaf(uint32_t sym)
+    __device__ __forceinline__ uint32_t find_leaf(uint32_t sym)
     {
         for (uint32_t r = 0; r * 64 <= kRoot; ++r) {
             const uint32_t p = r * 64 + lane;
@@ -682,7 +697,7 @@ struct Fgk {
     // update_fast; a level that reports there is walked again, the new path taking pv's role.
     // bounded: the encoder's pc_lb is current (pc_bound since the last insert): swaps below it
     // skip the cache scan
-    __device__ void walk(uint32_t s, uint32_t pv, bool bounded = false)
+    __device__ __forceinline__ void walk(uint32_t s, uint32_t pv, bool bounded = false)
     {
         for (;;) {
             const Wt v = T.wt[s + lane];  // sentinels cover s + 63 <= 575
@@ -806,14 +821,12 @@ template <int kSrc>
 __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t fin, RleCarry &cy,
                                               uint32_t *syms, uint32_t *scr, uint32_t lane)
 {
-    const uint32_t up = __shfl_up(x4, 1, 64);
-    const uint32_t xprev = (x4 << 8) | ((lane == 0 ? (cy.x << 24) : up) >> 24);
+    const uint32_t xprev = (x4 << 8) | (wave_shr1(x4, cy.x << 24) >> 24);
     // bytewise x - xprev (mod 256), SWAR
     const uint32_t c4 = kSrc == SRC_RAW_DIFF
                             ? (((x4 | 0x80808080u) - (xprev & 0x7F7F7F7Fu)) ^ ((x4 ^ ~xprev) & 0x80808080u))
                             : x4;
-    const uint32_t upc = __shfl_up(c4, 1, 64);
-    const uint32_t cprev = (c4 << 8) | ((lane == 0 ? (cy.c << 24) : upc) >> 24);
+    const uint32_t cprev = (c4 << 8) | (wave_shr1(c4, cy.c << 24) >> 24);
     const int i0 = (int)(lane * 4);
     uint32_t start[4], any = 0;
     int last = -1;
@@ -836,11 +849,11 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
         km[b] = k >= 258 ? k - 258 : k;
         R[b] = km[b] == 257 ? 0u : km[b] + 1;
     }
-    const uint32_t upR = __shfl_up(R[3], 1, 64);
+    const uint32_t upR = wave_shr1(R[3], cy.R);
     uint32_t n[4], s0[4], s1[4], tot = 0;
     for (uint32_t b = 0; b < 4; ++b) {
         const uint32_t i = (uint32_t)i0 + b;
-        const uint32_t rp = b ? R[b - 1] : (lane == 0 ? cy.R : upR);
+        const uint32_t rp = b ? R[b - 1] : upR;
         const uint32_t c = byte_of(c4, b);
         const uint32_t valid = i < m ? 1u : 0u;
         const uint32_t newrun = ((fin & (i + 1 == m ? 1u : 0u)) | (km[b] == 0 ? 1u : 0u));
@@ -1420,6 +1433,13 @@ struct BitSource {
             ridx = 0;
         }
     }
+    // the next 32 bits of the stream (decode_pair keeps the window itself)
+    __device__ __forceinline__ uint32_t take()
+    {
+        const uint32_t w = lane_read(chunk, ridx);
+        next_word();
+        return w;
+    }
     // push the next 32 bits (needs nwin <= 32)
     __device__ __forceinline__ void refill()
     {
@@ -1480,21 +1500,23 @@ __device__ __forceinline__ uint32_t fsm_apply(uint32_t f, uint32_t r) { return (
 __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCarry &cy, uint32_t dmask,
                                                  rsrc_t rs, uint32_t pos, uint32_t lane)
 {
-    const uint32_t up = __shfl_up(x4, 1, 64);
-    const uint32_t xp = (x4 << 8) | ((lane == 0 ? (cy.last << 24) : up) >> 24);  // previous symbols
+    const uint32_t xp = (x4 << 8) | (wave_shr1(x4, cy.last << 24) >> 24);  // previous symbols
     const uint32_t i0 = lane * 4;
     uint32_t f[4], F = kFid;
     for (uint32_t b = 0; b < 4; ++b) {
         f[b] = i0 + b < m ? (byte_of(x4, b) == byte_of(xp, b) ? kFeq : kFne) : kFid;
         F = fsm_compose(f[b], F);
     }
-    uint32_t inc = F;  // inclusive scan: lanes 0..l applied in order
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t g = __shfl_up(inc, off, 64);
-        inc = lane >= off ? fsm_compose(inc, g) : inc;
-    }
-    const uint32_t ex = __shfl_up(inc, 1, 64);
-    uint32_t r = fsm_apply(lane == 0 ? kFid : ex, cy.r);
+    // inclusive scan, lanes 0..l applied in order: DPP row shifts, then row broadcasts 15 and 31;
+    // lanes without a source keep the identity
+    uint32_t inc = F;
+    inc = fsm_compose(inc, __builtin_amdgcn_update_dpp(kFid, inc, 0x111, 0xF, 0xF, false));  // row_shr:1
+    inc = fsm_compose(inc, __builtin_amdgcn_update_dpp(kFid, inc, 0x112, 0xF, 0xF, false));  // row_shr:2
+    inc = fsm_compose(inc, __builtin_amdgcn_update_dpp(kFid, inc, 0x114, 0xF, 0xF, false));  // row_shr:4
+    inc = fsm_compose(inc, __builtin_amdgcn_update_dpp(kFid, inc, 0x118, 0xF, 0xF, false));  // row_shr:8
+    inc = fsm_compose(inc, __builtin_amdgcn_update_dpp(kFid, inc, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    inc = fsm_compose(inc, __builtin_amdgcn_update_dpp(kFid, inc, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    uint32_t r = fsm_apply(wave_shr1(inc, kFid), cy.r);
     uint32_t len[4], c[4], tot = 0, ds = 0, cnt_b = 4;  // cnt_b: the lane's count symbol (4: none)
     for (uint32_t b = 0; b < 4; ++b) {
         const uint32_t sb = byte_of(x4, b), pb = byte_of(xp, b);
@@ -1509,11 +1531,7 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
     }
     // exclusive scans of (length, diff sum mod 256), packed: both halves stay below 2^16
     const uint32_t mine = tot | ((ds & 255u) << 16);
-    uint32_t acc = mine;
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t g = __shfl_up(acc, off, 64);
-        acc += lane >= off ? g : 0u;
-    }
+    const uint32_t acc = RecSink::scan_add(mine);
     const uint32_t exc = acc - mine;
     uint32_t prev = (cy.prev + (exc >> 16)) & 255u;
     uint32_t o = pos + (exc & 0xFFFFu);
@@ -1547,6 +1565,292 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
     return all & 0xFFFFu;
 }
 
+// One stream's decoder (huffman.cpp:60-93 + transform.cpp:386-406 per symbol, then the RLE and
+// diff revert of transform.cpp:137-159 / 231-239 per 256-symbol block; header main.cpp:90-104).
+// decode_kernel runs one per wavefront; decode2_kernel runs two per wavefront in its hot loop
+// (decode_pair) and this one-stream code for everything that leaves it.
+template <int kW, int kDst>
+struct Dec {
+    // symbol indices: 32-bit below 2^32 symbols (narrow / wide), 64-bit for the huge layout
+    using Idx = std::conditional_t<kW == 2, uint64_t, uint32_t>;
+    Fgk<kW, true> fgk;
+    BitSource in;
+    uint32_t lane, sid, st, dmask;
+    uint64_t len, cap, payload_bits;
+    uint64_t obase;  // output window at byte obase (slides with the output, like the input's)
+    uint64_t pos;    // output bytes produced
+    rsrc_t rout;
+    RevCarry rc;
+    uint8_t *sbuf;  // this block's symbols (LDS)
+    Idx n;
+    uint64_t pacc = 0;  // HC_PROF regions
+
+    __device__ __forceinline__ Dec(Tree<kW, true> &t, uint32_t l) : fgk(t, l), lane(l) {}
+
+    // the stream's header; false: nothing to decode here (its error status is written, or another
+    // tree layout's launch owns it)
+    __device__ __forceinline__ bool open(const Batch &bt, uint32_t s)
+    {
+        sid = s;
+        const uint64_t in_off = uni64(bt.in_offs[sid]);
+        len = uni64(bt.in_lens[sid]);
+        cap = uni64(bt.out_caps[sid]);
+        const uint32_t len32 = (uint32_t)min(len, (uint64_t)kMaxBufBytes);
+        const rsrc_t rin = make_rsrc(bt.in + in_off, (len32 + 3u) & ~3u);
+        const uint32_t hdr = buf_load(rin, lane * 4);  // words 0..63 of the stream
+        st = 0;
+        uint64_t count = 0;
+        uint32_t flags = 0;
+        if (len < 9) {
+            st = HC_ERR_HEADER;  // main.cpp:99-104
+        } else {
+            count = (uint64_t)lane_read(hdr, 0) | ((uint64_t)lane_read(hdr, 1) << 32);
+            flags = lane_read(hdr, 2) & 255u;
+            const uint64_t avail = (len - 9) * 8;
+            // the first symbol costs >= 8 bits and each later one >= 1: a larger count cannot
+            // decode, and the reference ends such a stream with status 9 (transform.cpp:394-398)
+            if (count > (avail >= 8 ? avail - 7 : 0)) st = HC_ERR_HUFFMAN;
+            else if (kDst == DST_RAW && (flags & 0x40u)) st = HC_ERR_UNSUPPORTED;
+        }
+        if (st == 0 && tree_kind(count, bt.min_tree) != (uint32_t)kW) return false;  // another layout's launch owns it
+        if (st != 0) {
+            if (kW == 0 && lane == 0) {
+                bt.status[sid] = (int32_t)st;
+                bt.out_lens[sid] = 0;
+            }
+            return false;
+        }
+        in.rs = rin;
+        in.ibase = 0;
+        in.lane = lane;
+        in.cbase = 0;
+        in.chunk = __builtin_bswap32(hdr);
+        in.nxt = buf_load(rin, 256 + lane * 4);
+        in.ridx = 2;
+        in.win = 0;
+        in.nwin = 0;
+        in.refill();  // word 2: flags byte + first payload bits
+        in.win <<= 8;
+        in.nwin -= 8;
+        rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
+        obase = 0;
+        pos = 0;
+        dmask = kDst == DST_RAW && (flags & 0x80u) ? 255u : 0u;  // diff model
+        rc = {0, 0, 0};
+        sbuf = reinterpret_cast<uint8_t *>(fgk.T.syms);
+        n = (Idx)count;
+        payload_bits = (len - 9) * 8;
+        return true;
+    }
+    // input and output fit one buffer window (every batch stream): no window bookkeeping
+    __device__ __forceinline__ bool one_window() const
+    {
+        const uint32_t window = window_bytes();
+        return len + 512 <= window && cap <= window;
+    }
+    // bits read from the stream = words pushed into the window * 32 - bits still in it; the
+    // payload starts at bit 72. A stream that ends early decodes zero bits past its end (the
+    // range check); the reference stops there with status 9 (transform.cpp:394-398), which is
+    // what close() reports.
+    __device__ __forceinline__ uint64_t consumed() const { return ((in.ibase + in.cbase) / 4 + in.ridx) * 32 - in.nwin - 72; }
+    __device__ __forceinline__ bool stopped() const { return fgk.bad || consumed() > payload_bits + 64; }
+    // a block's symbols end at i1
+    __device__ __forceinline__ Idx block_end(Idx i0) const
+    {
+        if constexpr (kW == 2) return n - i0 < 256 ? n : i0 + 256;
+        else return min(n, i0 + 256);
+    }
+
+    template <bool kWin>
+    __device__ __forceinline__ void block_start(const Batch &bt, Idx i0)
+    {
+        if constexpr (kWin) {
+            const uint32_t window = window_bytes();
+            if (in.cbase >= window) {  // slide the input window to the current chunk (a block of
+                in.ibase += in.cbase;  // 256 symbols reads < 2 KB, so offsets stay below 2^31)
+                in.cbase = 0;
+                const uint64_t l = uni64(bt.in_lens[sid]);
+                in.rs = make_rsrc(bt.in + uni64(bt.in_offs[sid]) + in.ibase,
+                                  (uint32_t)min((l - min(l, in.ibase) + 3u) & ~3ull, (uint64_t)kMaxBufBytes));
+            }
+            if (pos - obase >= window) {  // and the output window to the next byte
+                obase = pos;
+                rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]) + obase,
+                                 obase < cap ? (uint32_t)min(cap - obase, (uint64_t)kMaxBufBytes) : 0u);
+            }
+        }
+        prio_by_progress(i0, n);
+    }
+
+    // symbol i - 1 (of the block at i0) left the hot loop with its leaf entry's position x and
+    // depth d, the body b read at x, the root path pv and the first level k whose leader test
+    // failed (the window stands d bits into its code): finish it
+    __device__ __forceinline__ void finish_symbol(uint32_t b, uint32_t pv, uint32_t k, uint32_t d, uint32_t x, Idx i, Idx i0)
+    {
+        if (!(b & (kInner | kNyt))) {  // a leaf whose update reported level k: walk from there
+            HC_PROF_BEGIN();
+            fgk.walk(lane_read(pv, k), pv);
+            HC_PROF_END(1);
+            return;
+        }
+        // nothing was stored for it
+        uint32_t sym = 0;
+        bool deep = false;  // a code longer than the cache's 9 levels: a rare symbol
+        HC_PROF_BEGIN();
+        if (b & kInner) {
+            // the code is longer than the tables reach, or they stopped short (a leaf that
+            // split since): descend bit by bit, top-down first (depth j at lane 64-j),
+            // then turned bottom-up
+            uint32_t depth = d;
+            fgk.stale += depth < 8 ? 1u : 0u;
+            if (fgk.stale >= kRefresh) fgk.from = 0;
+            // levels 1..8 of the prefix, lane 64 - j <- level j (lane 8 - j of the path read)
+            uint32_t pt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 56) & 63u) * 4), (int)pv);
+            do {
+                x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
+                pt = lane == 63 - depth ? x : pt;
+                ++depth;
+                b = uni(fgk.T.body[x]);
+            } while ((b & kInner) && depth < 63);
+            if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
+            deep = depth > kInsertDepth;
+            pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
+            pv = lane < depth ? pv : kRoot;
+            sym = b & 255u;
+        }
+        if (b & kNyt) {  // the new leaf below the NYT becomes level 0
+            sym = in.bits8();
+            // huffman.cpp:95-111 splits only for a symbol without a leaf; a corrupted stream
+            // can name a known one, whose own leaf is then updated
+            const uint32_t known = fgk.find_leaf(sym);
+            if (known == 0xFFFFFFFFu) {
+                x = uni(fgk.split(sym));
+                pv = __shfl_up(pv, 1, 64);
+                pv = lane == 0 ? x : pv;
+            } else {
+                fgk.chase(known, pv);
+            }
+        }
+        HC_PROF_END(2);
+        if (!(b & kInner)) {
+            HC_PROF_BEGIN();
+            // a rare symbol's leaf nearly always ties with the next position (9 in 10 on
+            // the slot-form model): walk from the leaf at once
+            if (deep) fgk.walk(lane_read(pv, 0), pv);
+            else fgk.update_path(pv);
+            HC_PROF_END(3);
+        }
+        sbuf[i - 1 - i0] = (uint8_t)sym;
+    }
+
+    // symbols i .. i1 - 1 of the block at i0, one stream
+    __device__ __forceinline__ void decode(Idx i0, Idx &i, Idx i1)
+    {
+        while (i < i1) {
+            // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
+            // where the walk from the root stops (depth d <= 8), the levels above give the
+            // positions the walk passes.
+            if (fgk.from < 9) {
+                HC_PROF_BEGIN();
+                fgk.build_levels();
+                HC_PROF_END(5);
+            }
+            if (in.nwin <= 32) in.refill();
+            // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
+            // symbol's depth is known the next symbol's table entry is read, before this
+            // symbol's update (the tables and body[] change only on the paths that leave the
+            // loop, and the loop is re-entered after them). Anything else
+            // (a longer code or a stale table: body inner; the NYT; a failed leader test) is
+            // forced to fail at level 0 so nothing is stored, and is finished outside.
+            // lane k reads level 8 - k's entry for the code's 8-bit prefix v, at
+            // ((256 | v) >> k) - 2: levels >= d repeat the leaf's entry (position | depth d), so
+            // lanes 0..8-d hold the leaf, lanes 9-d..7 its ancestors (level 8-k), lane 8 and up
+            // the root pad (lvl_root). One read gives the depth (lane 0) and the whole root path
+            // (duplicated lanes store the same word); it depends only on the window, so the next
+            // code's read goes out as soon as this code's depth is known.
+            // ((256 | v) >> k) - 2 = (v >> k) + (256 >> k) - 2, and v >> k = window bits 56 + k..63:
+            // one per-lane shift of the window's high word and one per-lane base; lanes 8 and up
+            // shift by 31 and land on lvl_root[-2 + 0/1] (both the root)
+            const uint32_t vsh = 24 + min(lane, 7u);
+            const uint32_t vbase = lds_off16(&fgk.T.lvl[0]) + 2 * (lane < 8 ? (256u >> lane) - 2 : 0xFFFFFFFEu);
+            auto path_read = [&](uint64_t w) __attribute__((always_inline)) {
+                return opaque(*(const lds_u16 *)(size_t)(vbase + ((uint32_t)(w >> 32) >> vsh) * 2));
+            };
+            uint32_t pr = path_read(in.win);
+            const uint32_t bbase = lds_off16(&fgk.T.body[0]);
+            uint32_t d, x, b, pv, k;
+            // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
+            // both sign bits set, one scalar AND
+            int32_t left = (int32_t)(i - i1);
+            lds_u8 *so = (lds_u8 *)sbuf + (uint32_t)(i - i0);  // the symbol's byte (LDS address in a VGPR)
+            asm("" : "+v"(so));
+            do {
+                const uint32_t e8 = uni(pr);  // the leaf's entry
+                x = e8 & 1023u;
+                d = e8 >> 10;
+                b = opaque(*(const lds_u16 *)(size_t)lshl1_add(x, bbase));
+                pv = pr & 1023u;
+                in.win <<= d;
+                in.nwin -= d;  // >= 25
+                uint32_t prn;
+                // a leaf's body is its symbol; inner / NYT (bit 15): force the failure
+                const uint32_t force = (uint32_t)__builtin_amdgcn_sbfe((int)b, 15, 1);
+                k = fgk.update_fast(pv, [&] { prn = path_read(in.win); }, force);  // the next code's
+                *so++ = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
+                ++left;
+                if (in.nwin <= 32) in.refill();
+                pr = prn;
+            } while ((int32_t)(k & (uint32_t)left) < 0);
+            i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
+            if (k == 0xFFFFFFFFu) continue;
+            // symbol i - 1 left the loop: the window stands d bits into its code
+            finish_symbol(uni(b), pv, k, uni(d), uni(x), i, i0);
+        }
+    }
+
+    // the block's symbols [i0, i1) leave: reverted to bytes (transform.cpp:137-159, 231-239) or
+    // stored as they are (the adaptive path's symbol stream)
+    __device__ __forceinline__ void close_block(Idx i0, Idx i1)
+    {
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t x4 = fgk.T.syms[lane];
+        const uint32_t m = (uint32_t)(i1 - i0);
+        if (kDst == DST_SYMBOLS) {
+            for (uint32_t b = 0; b < 4; ++b)
+                buf_store8(rout, lane * 4 + b < m ? (uint32_t)(pos - obase) + lane * 4 + b : kDrop, byte_of(x4, b));
+            pos += m;
+        } else {
+            HC_PROF_BEGIN();
+            pos += revert_block(x4, m, rc, dmask, rout, (uint32_t)(pos - obase), lane);
+            HC_PROF_END(4);
+        }
+    }
+
+    // blocks from i0 on; a block left unfinished at i (i0 <= i < its end) is finished first
+    template <bool kWin>
+    __device__ __forceinline__ void run(const Batch &bt, Idx i0, Idx i)
+    {
+        for (; i0 < n; i0 += 256, i = i0) {
+            if (stopped()) break;
+            block_start<kWin>(bt, i0);
+            const Idx i1 = block_end(i0);
+            decode(i0, i, i1);
+            close_block(i0, i1);
+        }
+    }
+
+    __device__ __forceinline__ void close(const Batch &bt)
+    {
+        if (consumed() > payload_bits) st = HC_ERR_HUFFMAN;  // ran past the payload
+        if (fgk.bad) st = HC_ERR_DEVICE;
+        if (st == 0 && pos > cap) st = HC_ERR_CAPACITY;
+        if (lane == 0) {
+            bt.status[sid] = (int32_t)st;
+            bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? pos : 0;
+        }
+    }
+};
+
 template <int kW, int kDst>
 __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW>))) void decode_kernel(Batch bt)
 {
@@ -1556,238 +1860,190 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
     if (sid >= bt.n) return;
-    uint64_t pacc = 0;  // HC_PROF regions
-    (void)pacc;
-
-    const uint64_t in_off = uni64(bt.in_offs[sid]);
-    const uint64_t len = uni64(bt.in_lens[sid]);
-    const uint64_t cap = uni64(bt.out_caps[sid]);
-    const uint32_t len32 = (uint32_t)min(len, (uint64_t)kMaxBufBytes);
-    const rsrc_t rin = make_rsrc(bt.in + in_off, (len32 + 3u) & ~3u);
-    const uint32_t hdr = buf_load(rin, lane * 4);  // words 0..63 of the stream
-    uint32_t st = 0;
-    uint64_t count = 0;
-    uint32_t flags = 0;
-    if (len < 9) {
-        st = HC_ERR_HEADER;  // main.cpp:99-104
-    } else {
-        count = (uint64_t)lane_read(hdr, 0) | ((uint64_t)lane_read(hdr, 1) << 32);
-        flags = lane_read(hdr, 2) & 255u;
-        const uint64_t avail = (len - 9) * 8;
-        // the first symbol costs >= 8 bits and each later one >= 1: a larger count cannot
-        // decode, and the reference ends such a stream with status 9 (transform.cpp:394-398)
-        if (count > (avail >= 8 ? avail - 7 : 0)) st = HC_ERR_HUFFMAN;
-        else if (kDst == DST_RAW && (flags & 0x40u)) st = HC_ERR_UNSUPPORTED;
-    }
-    if (st == 0 && tree_kind(count, bt.min_tree) != (uint32_t)kW) return;  // another layout's launch owns it
-    if (st != 0) {
-        if (kW == 0 && lane == 0) {
-            bt.status[sid] = (int32_t)st;
-            bt.out_lens[sid] = 0;
-        }
-        return;
-    }
-
-    Fgk<kW, true> fgk(trees[wv], lane);
-    BitSource in;
-    in.rs = rin;
-    in.ibase = 0;
-    in.lane = lane;
-    const uint32_t window = window_bytes();
-    in.cbase = 0;
-    in.chunk = __builtin_bswap32(hdr);
-    in.nxt = buf_load(rin, 256 + lane * 4);
-    in.ridx = 2;
-    in.win = 0;
-    in.nwin = 0;
-    in.refill();  // word 2: flags byte + first payload bits
-    in.win <<= 8;
-    in.nwin -= 8;
-
-    // output window at byte obase (slides with the output, like the input's)
-    rsrc_t rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]), (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
-    uint64_t obase = 0;
-    uint64_t pos = 0;  // output bytes produced
-    const uint32_t dmask = kDst == DST_RAW && (flags & 0x80u) ? 255u : 0u;  // diff model
-    RevCarry rc = {0, 0, 0};
-    uint8_t *const sbuf = reinterpret_cast<uint8_t *>(fgk.T.syms);  // this block's symbols
-    // symbol indices: 32-bit below 2^32 symbols (narrow / wide), 64-bit for the huge layout
-    using Idx = std::conditional_t<kW == 2, uint64_t, uint32_t>;
-    const Idx n = (Idx)count;
-    // bits read from the stream = words pushed into the window * 32 - bits still in it; the
-    // payload starts at bit 72. A stream that ends early decodes zero bits past its end (the
-    // range check); the reference stops there with status 9 (transform.cpp:394-398), which is
-    // what the comparison after the loop reports.
-    const uint64_t payload_bits = (len - 9) * 8;
-    auto consumed = [&]() __attribute__((always_inline)) -> uint64_t {
-        return ((in.ibase + in.cbase) / 4 + in.ridx) * 32 - in.nwin - 72;
-    };
-
+    Dec<kW, kDst> dec(trees[wv], lane);
+    if (!dec.open(bt, sid)) return;
     // two copies of the block loop, as in the encoder: without window bookkeeping for streams
     // that fit one window (input and output), with it for the rest
-    auto blocks = [&](auto windowed) __attribute__((always_inline)) {
-        constexpr bool kWin = decltype(windowed)::value;
-        for (Idx i0 = 0; i0 < n; i0 += 256) {
-            if (fgk.bad || consumed() > payload_bits + 64) break;
-            if constexpr (kWin) {
-                if (in.cbase >= window) {  // slide the input window to the current chunk (a block of
-                    in.ibase += in.cbase;  // 256 symbols reads < 2 KB, so offsets stay below 2^31)
-                    in.cbase = 0;
-                    const uint64_t l = uni64(bt.in_lens[sid]);
-                    in.rs = make_rsrc(bt.in + uni64(bt.in_offs[sid]) + in.ibase,
-                                      (uint32_t)min((l - min(l, in.ibase) + 3u) & ~3ull, (uint64_t)kMaxBufBytes));
-                }
-                if (pos - obase >= window) {  // and the output window to the next byte
-                    obase = pos;
-                    rout = make_rsrc(bt.out + uni64(bt.out_offs[sid]) + obase,
-                                     obase < cap ? (uint32_t)min(cap - obase, (uint64_t)kMaxBufBytes) : 0u);
-                }
-            }
-            prio_by_progress(i0, n);
-            Idx i1;
-            if constexpr (kW == 2) i1 = n - i0 < 256 ? n : i0 + 256;
-            else i1 = min(n, i0 + 256);
-            Idx i = i0;
-            while (i < i1) {
-                // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
-                // where the walk from the root stops (depth d <= 8), the levels above give the
-                // positions the walk passes.
-                if (fgk.from < 9) {
-                    HC_PROF_BEGIN();
-                    fgk.build_levels();
-                    HC_PROF_END(5);
-                }
-                if (in.nwin <= 32) in.refill();
-                // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
-                // symbol's depth is known the next symbol's table entry is read, before this
-                // symbol's update (the tables and body[] change only on the paths that leave the
-                // loop, and the loop is re-entered after them). Anything else
-                // (a longer code or a stale table: body inner; the NYT; a failed leader test) is
-                // forced to fail at level 0 so nothing is stored, and is finished outside.
-                // lane k reads level 8 - k's entry for the code's 8-bit prefix v, at
-                // ((256 | v) >> k) - 2: levels >= d repeat the leaf's entry (position | depth d), so
-                // lanes 0..8-d hold the leaf, lanes 9-d..7 its ancestors (level 8-k), lane 8 and up
-                // the root pad (lvl_root). One read gives the depth (lane 0) and the whole root path
-                // (duplicated lanes store the same word); it depends only on the window, so the next
-                // code's read goes out as soon as this code's depth is known.
-                // ((256 | v) >> k) - 2 = (v >> k) + (256 >> k) - 2, and v >> k = window bits 56 + k..63:
-                // one per-lane shift of the window's high word and one per-lane base; lanes 8 and up
-                // shift by 31 and land on lvl_root[-2 + 0/1] (both the root)
-                const uint32_t vsh = 24 + min(lane, 7u);
-                const uint32_t vbase = lds_off16(&fgk.T.lvl[0]) + 2 * (lane < 8 ? (256u >> lane) - 2 : 0xFFFFFFFEu);
-                auto path_read = [&](uint64_t w) __attribute__((always_inline)) {
-                    return opaque(*(const lds_u16 *)(size_t)(vbase + ((uint32_t)(w >> 32) >> vsh) * 2));
-                };
-                uint32_t pr = path_read(in.win);
-                const uint32_t bbase = lds_off16(&fgk.T.body[0]);
-                uint32_t d, x, b, pv, k;
-                // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
-                // both sign bits set, one scalar AND
-                int32_t left = (int32_t)(i - i1);
-                lds_u8 *so = (lds_u8 *)sbuf + (uint32_t)(i - i0);  // the symbol's byte (LDS address in a VGPR)
-                asm("" : "+v"(so));
-                do {
-                    const uint32_t e8 = uni(pr);  // the leaf's entry
-                    x = e8 & 1023u;
-                    d = e8 >> 10;
-                    b = opaque(*(const lds_u16 *)(size_t)lshl1_add(x, bbase));
-                    pv = pr & 1023u;
-                    in.win <<= d;
-                    in.nwin -= d;  // >= 25
-                    uint32_t prn;
-                    // a leaf's body is its symbol; inner / NYT (bit 15): force the failure
-                    const uint32_t force = (uint32_t)__builtin_amdgcn_sbfe((int)b, 15, 1);
-                    k = fgk.update_fast(pv, [&] { prn = path_read(in.win); }, force);  // the next code's
-                    *so++ = (uint8_t)b;  // the symbol (a leaf's body); rewritten when it leaves
-                    ++left;
-                    if (in.nwin <= 32) in.refill();
-                    pr = prn;
-                } while ((int32_t)(k & (uint32_t)left) < 0);
-                i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
-                if (k == 0xFFFFFFFFu) continue;
-                // symbol i - 1 left the loop: the window stands d bits into its code
-                b = uni(b);
-                if (!(b & (kInner | kNyt))) {  // a leaf whose update reported level k: walk from there
-                    HC_PROF_BEGIN();
-                    fgk.walk(lane_read(pv, k), pv);
-                    HC_PROF_END(1);
-                    continue;
-                }
-                // nothing was stored for it
-                uint32_t sym = 0;
-                bool deep = false;  // a code longer than the cache's 9 levels: a rare symbol
-                HC_PROF_BEGIN();
-                if (b & kInner) {
-                    // the code is longer than the tables reach, or they stopped short (a leaf that
-                    // split since): descend bit by bit, top-down first (depth j at lane 64-j),
-                    // then turned bottom-up
-                    uint32_t depth = uni(d);
-                    x = uni(x);
-                    fgk.stale += depth < 8 ? 1u : 0u;
-                    if (fgk.stale >= kRefresh) fgk.from = 0;
-                    // levels 1..8 of the prefix, lane 64 - j <- level j (lane 8 - j of the path read)
-                    uint32_t pt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 56) & 63u) * 4), (int)pv);
-                    do {
-                        x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
-                        pt = lane == 63 - depth ? x : pt;
-                        ++depth;
-                        b = uni(fgk.T.body[x]);
-                    } while ((b & kInner) && depth < 63);
-                    if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
-                    deep = depth > kInsertDepth;
-                    pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
-                    pv = lane < depth ? pv : kRoot;
-                    sym = b & 255u;
-                }
-                if (b & kNyt) {  // the new leaf below the NYT becomes level 0
-                    sym = in.bits8();
-                    // huffman.cpp:95-111 splits only for a symbol without a leaf; a corrupted stream
-                    // can name a known one, whose own leaf is then updated
-                    const uint32_t known = fgk.find_leaf(sym);
-                    if (known == 0xFFFFFFFFu) {
-                        x = uni(fgk.split(sym));
-                        pv = __shfl_up(pv, 1, 64);
-                        pv = lane == 0 ? x : pv;
-                    } else {
-                        fgk.chase(known, pv);
-                    }
-                }
-                HC_PROF_END(2);
-                if (!(b & kInner)) {
-                    HC_PROF_BEGIN();
-                    // a rare symbol's leaf nearly always ties with the next position (9 in 10 on
-                    // the slot-form model): walk from the leaf at once
-                    if (deep) fgk.walk(lane_read(pv, 0), pv);
-                    else fgk.update_path(pv);
-                    HC_PROF_END(3);
-                }
-                sbuf[i - 1 - i0] = (uint8_t)sym;
-            }
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t x4 = fgk.T.syms[lane];
-            const uint32_t m = (uint32_t)(i1 - i0);
-            if (kDst == DST_SYMBOLS) {
-                for (uint32_t b = 0; b < 4; ++b)
-                    buf_store8(rout, lane * 4 + b < m ? (uint32_t)(pos - obase) + lane * 4 + b : kDrop, byte_of(x4, b));
-                pos += m;
-            } else {
-                HC_PROF_BEGIN();
-                pos += revert_block(x4, m, rc, dmask, rout, (uint32_t)(pos - obase), lane);
-                HC_PROF_END(4);
-            }
-        }
-    };
-    if (len + 512 <= window && cap <= window) blocks(std::false_type{});
-    else blocks(std::true_type{});
-    if (consumed() > payload_bits) st = HC_ERR_HUFFMAN;  // ran past the payload
-    if (fgk.bad) st = HC_ERR_DEVICE;
-    if (st == 0 && pos > cap) st = HC_ERR_CAPACITY;
-    if (lane == 0) {
-        bt.status[sid] = (int32_t)st;
-        bt.out_lens[sid] = (st == 0 || st == HC_ERR_CAPACITY) ? pos : 0;
-    }
+    if (dec.one_window()) dec.template run<false>(bt, 0, 0);
+    else dec.template run<true>(bt, 0, 0);
+    dec.close(bt);
     trace_wave(sid, t0, lane);
-    prof_store(sid, t0, pacc + fgk.pacc, lane);
+    prof_store(sid, t0, dec.pacc + dec.fgk.pacc, lane);
+}
+
+// ---------------------------------------------------------- two streams per wavefront --
+
+// decode_pair: the hot loop of Dec::decode for two narrow streams at once, A on lanes 0-31 and B
+// on lanes 32-63, each half reading its own LDS tree. Everything the one-stream loop keeps in
+// scalar registers per stream (the bit window and its fill, the code's leaf entry and depth) is
+// held per half in vector registers, so that one vector instruction serves both streams; what
+// stays scalar (the symbol count, the two store masks, the loop test) is shared.
+//  * Lane l of a half reads, like lane k = l & 15 of the one-stream loop, level 8 - k's table
+//    entry for the code's 8-bit prefix (k >= 8: the root pad); lanes 16-30 repeat lanes 0-14, so
+//    the leaf's entry sits in lanes 0 and 16 of the half and one row_newbcast DPP move gives it to
+//    every lane. Lanes 0-15 of a half are the one-stream loop's path vector.
+//  * Lane 31 of each half reads a guard pad (the decoder's unused where[]: kMissPos twice) whose
+//    weight pair (all ones - 1, 0) fails every leader test, so each half's failure mask is never
+//    empty: the store masks of both halves are the one 64-bit (fail - (1 | 1 << 32)) & ~fail, and
+//    a real failure is any bit but the two guards.
+//  * Every lane of a half reads the leaf's body (one broadcast address) and folds it into the
+//    test (force: all lanes of the half fail, the first at level 0); lanes 0 / 32 store the
+//    symbol byte.
+// The loop leaves when a real level fails in either half (that half's symbol is finished by
+// Dec::finish_symbol; the other half's symbol is complete) or at the end of the block.
+template <int kDst>
+__device__ __forceinline__ void decode_pair(Dec<0, kDst> &A, Dec<0, kDst> &B, uint32_t i0, uint32_t &i, uint32_t i1)
+{
+    const uint32_t lane = A.lane, hl = lane & 31u, k = lane & 15u;
+    const bool hb = lane >= 32;  // lanes of stream B
+    constexpr uint64_t kGuard = 0x8000000080000000ull;
+    // per-lane LDS bases of the lane's half
+    const uint32_t lvl = hb ? lds_off16(&B.fgk.T.lvl[0]) : lds_off16(&A.fgk.T.lvl[0]);
+    const uint32_t guard = hb ? lds_off16(&B.fgk.T.where[0]) : lds_off16(&A.fgk.T.where[0]);
+    const uint32_t vbody = hb ? lds_off16(&B.fgk.T.body[0]) : lds_off16(&A.fgk.T.body[0]);
+    const uint32_t vwt = hb ? lds_off(&B.fgk.T.wt[0]) : lds_off(&A.fgk.T.wt[0]);
+    const uint32_t vscr = hb ? lds_off(&B.fgk.T.scratch[hl]) : lds_off(&A.fgk.T.scratch[hl]);
+    const uint32_t vsyms = hb ? lds_off(&B.fgk.T.syms[0]) : lds_off(&A.fgk.T.syms[0]);
+    const uint32_t vsh = hl == 31 ? 31u : 24 + min(k, 7u);
+    const uint32_t vbase = hl == 31 ? guard : lvl + 2 * (k < 8 ? (256u >> k) - 2 : 0xFFFFFFFEu);
+    // masks held in scalar registers across the loop (left alone, the compiler rebuilds them
+    // from immediates on every symbol)
+    uint64_t klead = 0x0000000100000001ull, kreal = ~kGuard;
+    asm volatile("" : "+s"(klead), "+s"(kreal));
+    while (i < i1) {
+        if (A.fgk.from < 9) A.fgk.build_levels();
+        if (B.fgk.from < 9) B.fgk.build_levels();
+        if (A.in.nwin <= 32) A.in.refill();
+        if (B.in.nwin <= 32) B.in.refill();
+        // the halves' windows
+        uint64_t vwin = hb ? B.in.win : A.in.win;
+        uint32_t vnwin = hb ? B.in.nwin : A.in.nwin;
+        asm volatile("" : "+v"(vwin), "+v"(vnwin));
+        auto path_read = [&](uint64_t w) __attribute__((always_inline)) {
+            return opaque(*(const lds_u16 *)(size_t)(vbase + ((uint32_t)(w >> 32) >> vsh) * 2));
+        };
+        uint32_t pr = path_read(vwin);
+        uint32_t so = vsyms + (i - i0);  // the symbol's byte in the half's block
+        asm volatile("" : "+v"(so));
+        uint32_t e8, b, pv, kf;
+        uint64_t fail;
+        // loop while no real level failed (kf = 0xFFFFFFFF) and symbols are left (left < 0): both
+        // sign bits set, one scalar AND
+        int32_t left = (int32_t)(i - i1);
+        do {
+            e8 = (uint32_t)__builtin_amdgcn_mov_dpp((int)pr, 0x150, 0xF, 0xF, false);  // row_newbcast:0
+            const uint32_t d = e8 >> 10;
+            pv = pr & 1023u;
+            // the leaf's body, the same address in every lane of the half (a broadcast read)
+            b = opaque(*(const lds_u16 *)(size_t)(vbody + (e8 & 1023u) * 2));
+            const uint32_t wa = vwt + pv * 4;
+            const uint32_t w0 = *(const lds_u32 *)(size_t)wa, w1 = *(const lds_u32 *)(size_t)(wa + 4);
+            vwin <<= d;
+            vnwin -= d;
+            const uint32_t prn = path_read(vwin);  // the next code's
+            const uint32_t nv = w0 + 1024u;
+            // a leaf's body is its symbol; inner / NYT (bit 15): every lane of the half fails
+            const uint32_t force = (uint32_t)__builtin_amdgcn_sbfe((int)b, 15, 1);
+            fail = ballot(w1 < (nv | force));
+            const uint64_t sm = (fail - klead) & ~fail;  // lanes below each half's first failure
+            *(lds_u32 *)(size_t)sel(sm, wa, vscr) = nv;
+            *(lds_u8 *)(size_t)sel(klead, so, vscr) = (uint8_t)b;  // the symbol; rewritten if it leaves
+            ++so;
+            ++left;
+            kf = ff1(fail & kreal);
+            const uint64_t rm = ballot(vnwin <= 32u);
+            if (rm) {  // a half's window needs its next word
+                const uint32_t wa32 = ((uint32_t)rm & 1u) ? A.in.take() : 0u;
+                const uint32_t wb32 = ((uint32_t)(rm >> 32) & 1u) ? B.in.take() : 0u;
+                const uint32_t w = hb ? wb32 : wa32;
+                vwin |= (uint64_t)w << ((32u - vnwin) & 63u);
+                vnwin = sel(rm, vnwin + 32u, vnwin);
+            }
+            pr = prn;
+        } while ((int32_t)(kf & (uint32_t)left) < 0);
+        i = (uint32_t)((int32_t)i1 + left);
+        A.in.win = uni64(vwin);
+        A.in.nwin = uni(vnwin);
+        B.in.win = (uint64_t)lane_read((uint32_t)vwin, 32) | ((uint64_t)lane_read((uint32_t)(vwin >> 32), 32) << 32);
+        B.in.nwin = lane_read(vnwin, 32);
+        const uint64_t real = fail & ~kGuard;
+#ifdef HC_PAIR_PRIO
+        if (real) __builtin_amdgcn_s_setprio(3);
+#endif
+        if ((uint32_t)real) {  // symbol i - 1 of A left the loop
+            const uint32_t pa = lane < 16 ? pv : kRoot;
+            A.finish_symbol(uni(b), pa, ff1(fail), uni(e8) >> 10, uni(e8) & 1023u, i, i0);
+        }
+        if (real >> 32) {  // ... of B: its path moved down to lanes 0-15
+            const uint32_t up = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 32) & 63u) * 4), (int)pv);
+            const uint32_t pb = lane < 16 ? up : kRoot;
+            const uint32_t eb = lane_read(e8, 32);
+            B.finish_symbol(lane_read(b, 32), pb, ff1(fail >> 32), eb >> 10, eb & 1023u, i, i0);
+        }
+#ifdef HC_PAIR_PRIO
+        if (real) prio_by_progress(i0, A.n);
+#endif
+    }
+}
+
+// Two narrow streams per wavefront (4 per SIMD: LDS holds 32 streams per CU either way): while
+// both have symbols, their blocks advance in lockstep through decode_pair (a symbol that leaves
+// the shared loop is finished by its stream alone, so the two stay at the same symbol index and
+// their 256-symbol blocks end together); then the longer one finishes alone (Dec::run). A stream
+// that another tree layout owns, or that fails its header, leaves its partner alone from the start.
+template <int kDst>
+__global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void decode2_kernel(Batch bt)
+{
+    __shared__ Tree<0, true> trees[2 * kWaves];
+    const uint32_t lane = lane_id();
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t sa = 2 * (blockIdx.x * kWaves + wv), sb = sa + 1;
+    if (sa >= bt.n) return;
+    Dec<0, kDst> A(trees[2 * wv], lane), B(trees[2 * wv + 1], lane);
+    const bool on_a = A.open(bt, sa);
+    const bool on_b = sb < bt.n && B.open(bt, sb);
+    uint32_t ia = 0, ib = 0;  // where each stream stands (the block of each is ia & ~255)
+    if (on_a && on_b && A.one_window() && B.one_window()) {
+        // guard pads for decode_pair's lane 31 of each half (the decoder leaves where[] unused)
+        *(lane < 2 ? &A.fgk.T.where[lane] : A.fgk.scr16()) = (uint16_t)kMissPos;
+        *(lane < 2 ? &B.fgk.T.where[lane] : B.fgk.scr16()) = (uint16_t)kMissPos;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nc = min(A.n, B.n);
+        uint32_t i = 0;
+        for (uint32_t i0 = 0; i0 < nc; i0 += 256) {
+            if (A.stopped() || B.stopped()) break;
+            A.template block_start<false>(bt, i0);
+            B.template block_start<false>(bt, i0);
+            const uint32_t i1 = min(nc, i0 + 256);
+            decode_pair(A, B, i0, i, i1);
+            if (i1 == A.block_end(i0)) A.close_block(i0, i1);
+            if (i1 == B.block_end(i0)) B.close_block(i0, i1);
+        }
+        ia = ib = i;
+    }
+    // the rest of each stream alone, from a block start or from inside the pair's last block
+    if (on_a) {
+        const uint32_t i0 = ia & ~255u;
+        if (ia > i0 && ia < A.block_end(i0)) {  // finish the pair's last block
+            A.decode(i0, ia, A.block_end(i0));
+            A.close_block(i0, A.block_end(i0));
+            ia = i0 + 256;
+        }
+        if (A.one_window()) A.template run<false>(bt, (ia + 255) & ~255u, (ia + 255) & ~255u);
+        else A.template run<true>(bt, (ia + 255) & ~255u, (ia + 255) & ~255u);
+        A.close(bt);
+    }
+    if (on_b) {
+        const uint32_t i0 = ib & ~255u;
+        if (ib > i0 && ib < B.block_end(i0)) {
+            B.decode(i0, ib, B.block_end(i0));
+            B.close_block(i0, B.block_end(i0));
+            ib = i0 + 256;
+        }
+        if (B.one_window()) B.template run<false>(bt, (ib + 255) & ~255u, (ib + 255) & ~255u);
+        else B.template run<true>(bt, (ib + 255) & ~255u, (ib + 255) & ~255u);
+        B.close(bt);
+    }
 }
 
 }  // namespace
@@ -1854,12 +2110,16 @@ hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)
     Batch b = b0;
     b.min_tree = min_tree();
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
+    const dim3 grid2((b.n + 2 * kWaves - 1) / (2 * kWaves));
+    const bool pair = dec_pair() != 0;
     if (dst == DST_RAW) {
-        decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
+        if (pair) decode2_kernel<DST_RAW><<<grid2, block, 0, st>>>(b);
+        else decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_RAW><<<grid, block, 0, st>>>(b);
     } else {
-        decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        if (pair) decode2_kernel<DST_SYMBOLS><<<grid2, block, 0, st>>>(b);
+        else decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
     }
@@ -1888,6 +2148,13 @@ extern "C" int hc_debug_set_enc_tab(uint32_t mode)
 {
     // 0: per stream (sampled alphabet), 1: path cache for every stream, 2: tables for every stream
     hc::g_enc_tab = mode > 2 ? 0 : mode;
+    return 0;
+}
+
+extern "C" int hc_debug_set_dec_pair(uint32_t on)
+{
+    // 1: narrow streams decode two per wavefront, 0: one per wavefront (default)
+    hc::g_dec_pair = on ? 1u : 0u;
     return 0;
 }
 
