@@ -1739,6 +1739,7 @@ constexpr uint64_t kParMin = 1ull << 20;  // block symbols from which a stream t
 // debug build: hc_debug_set_par_min lowers the threshold so that tests run the pass on small
 // streams (all of the serial pass's edge cases through the parallel one)
 __device__ uint64_t g_par_min = kParMin;
+static uint64_t g_par_min_host = kParMin;  // its host copy (adapt_decode_work_bound)
 __device__ __forceinline__ uint64_t par_min() { return g_par_min; }
 // hc_debug_set_par_skew: par_walk enters every odd chunk this many output bytes off its predicted
 // entry (mod W H), so tests exercise par_fix's re-runs and its repair of the starts[] entries a
@@ -3662,7 +3663,13 @@ uint64_t adapt_decode_work_bound(uint64_t total_in, uint64_t total_out, uint32_t
     // their window info (8 kZcap / kSub bytes: 4 at kZcap 1024), packed s0 0.25, records; 4992
     // bytes of rounding per stream
     constexpr uint64_t kPar8 = (8 * (8 * kZcap + kSub / 4 + 64) + kSub - 1) / kSub;  // per 8 symbols
-    return ws_header(n) + (8 + kPar8) * total_in + total_out / 4 + total_out / kChunk + 4992ull * n + 4096;
+    uint64_t tiny = 0;
+#ifdef HC_DEBUG_HOOKS
+    // the debug threshold below 2^20 symbols (hc_debug_set_par_min) sends tiny streams through
+    // the pass: each may need a whole sub-chunk's records, which the per-symbol term does not cover
+    if (g_par_min_host < kParMin) tiny = (8ull * kZcap + kSub / 4 + 256) * n;
+#endif
+    return ws_header(n) + (8 + kPar8) * total_in + total_out / 4 + total_out / kChunk + 4992ull * n + tiny + 4096;
 }
 
 // Diagnostic stage clock (debug build only, hc_debug_stage_clock / hc_debug_stage_times): when
@@ -3803,6 +3810,7 @@ extern "C" int hc_debug_set_par_skew(uint64_t bytes)
 extern "C" int hc_debug_set_par_min(uint64_t symbols)
 {
     // block symbols from which an adaptive stream's boundaries take the parallel pass
+    hc::g_par_min_host = symbols;
     return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_par_min), &symbols, sizeof(symbols)) == hipSuccess ? 0 : HC_ERR_DEVICE;
 }
 

@@ -159,6 +159,12 @@ constexpr uint32_t kInsertDepth = HC_INSERT_DEPTH;
 // encoder: a miss chases this many levels, then looks the position reached up in the path cache
 constexpr uint32_t kProbe = HC_PROBE;
 constexpr uint32_t kRow = 16;       // u16 per cache entry
+// 1: non-windowed streams keep four input chunks in flight instead of one. Measured (A/B, C5 -c
+// -m / grad): encode 513 / 2.85 ms against 508 / 2.89 ms with one; the three extra registers live
+// across the FGK loop cost more than the latency they hide.
+#ifndef HC_ENC_DEEP
+#define HC_ENC_DEEP 0
+#endif
 constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte chunk, <= 342
                                     // (a byte emits 2 only at a run start that follows a run of
                                     // >= 3, so such bytes are >= 3 apart)
@@ -815,17 +821,43 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t b) { return (w 
 // valid, fin says byte m-1 is the stream's last. Per byte: k = offset in its run (the run may
 // continue from the previous chunk), km = k mod 258, run counter R = km + 1 (0 at the cut);
 // a byte emits the previous run's count byte and itself when a run starts (or it is the final
-// byte), itself at km 1..2, 255 at km 257, nothing otherwise. Symbols go to syms[] in order;
-// returns how many.
+// byte), itself at km 1..2, 255 at km 257, nothing otherwise. The chunk's symbols are appended
+// to the at symbols pending in sb[] (room for cap); returns the symbols pending after the chunk,
+// or -- when they would not fit -- sets full, writes nothing and leaves the carry as it was (the
+// caller codes the pending symbols and runs the chunk again).
+// Fast path (rle_chunk_model.pure_chunk): a full, non-final chunk whose 256 transformed bytes all
+// continue the carried byte's run puts byte i at km = (R + i) mod 258, so it emits only the
+// events of the residues 257 (255), 0, 1, 2 (the byte) that fall on i <= 255: in byte order the
+// cyclic order 257, 0, 1, 2 rotated to start at R when R <= 2, lane j < 4 taking entry j.
 template <int kSrc>
-__device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t fin, RleCarry &cy,
-                                              uint32_t *syms, uint32_t *scr, uint32_t lane)
+__device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t fin, RleCarry &cy, uint8_t *sb,
+                                              uint32_t at, uint32_t cap, uint32_t *scr, uint32_t lane, uint32_t &full)
 {
     const uint32_t xprev = (x4 << 8) | (wave_shr1(x4, cy.x << 24) >> 24);
     // bytewise x - xprev (mod 256), SWAR
     const uint32_t c4 = kSrc == SRC_RAW_DIFF
                             ? (((x4 | 0x80808080u) - (xprev & 0x7F7F7F7Fu)) ^ ((x4 ^ ~xprev) & 0x80808080u))
                             : x4;
+    uint8_t *sc = reinterpret_cast<uint8_t *>(scr);
+    if (m == 256 && !fin && ballot(c4 != cy.c * 0x01010101u) == 0) {
+        const uint32_t R = cy.R;
+        const uint32_t rot = R <= 2 ? R + 1 : 0;
+        const uint32_t q = (lane + rot) & 3u;
+        const uint32_t e = q == 0 ? 257u : q - 1;
+        uint32_t i = e + 258 - R;
+        i = i >= 258 ? i - 258 : i;
+        const bool on = lane < 4 && i <= 255;
+        const uint32_t total = (uint32_t)__builtin_popcountll(ballot(on));
+        if (at + total > cap) {
+            full = 1;
+            return at;
+        }
+        *(on ? sb + at + lane : sc) = (uint8_t)(e == 257 ? 255u : cy.c);
+        __builtin_amdgcn_wave_barrier();
+        cy.x = lane_read(x4, 63) >> 24;
+        cy.R = R + 256 >= 258 ? R - 2 : R + 256;
+        return at + total;
+    }
     const uint32_t cprev = (c4 << 8) | (wave_shr1(c4, cy.c << 24) >> 24);
     const int i0 = (int)(lane * 4);
     uint32_t start[4], any = 0;
@@ -871,23 +903,25 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
         const uint64_t bm = ballot((tot >> p) & 1u);
         basepos += __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << p;
     }
-    uint8_t *sb = reinterpret_cast<uint8_t *>(syms);
-    uint8_t *sc = reinterpret_cast<uint8_t *>(scr);
-    uint32_t o = basepos;
+    const uint32_t total = lane_read(basepos + tot, 63);
+    if (at + total > cap) {
+        full = 1;
+        return at;
+    }
+    uint32_t o = at + basepos;
     for (uint32_t b = 0; b < 4; ++b) {
         *(n[b] >= 1 ? sb + o : sc) = (uint8_t)s0[b];
         *(n[b] == 2 ? sb + o + 1 : sc + 1) = (uint8_t)s1[b];
         o += n[b];
     }
     __builtin_amdgcn_wave_barrier();
-    const uint32_t total = lane_read(basepos + tot, 63);
     // carries: the chunk's last byte
     const uint32_t L = m - 1, ll = L >> 2, lb = L & 3u;
     const uint32_t rl = lb == 0 ? R[0] : (lb == 1 ? R[1] : (lb == 2 ? R[2] : R[3]));
     cy.x = byte_of(lane_read(x4, ll), lb);
     cy.c = byte_of(lane_read(c4, ll), lb);
     cy.R = lane_read(rl, ll);
-    return total;
+    return at + total;
 }
 
 // ------------------------------------------------------------------------- output stage --
@@ -1108,6 +1142,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // through the sink and re-bases koff. Positions stay in range by construction, so `bad` (a
     // bug detector) is checked once per chunk.
     const uint8_t *const sb = reinterpret_cast<const uint8_t *>(fgk.T.syms);
+    uint8_t *const sb_w = reinterpret_cast<uint8_t *>(fgk.T.syms);
     auto miss = [&](uint32_t sv) {
         const uint32_t sym = uni(sv);
         uint32_t s = uni(fgk.T.where[sym]) & 1023u;
@@ -1357,39 +1392,81 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     uint32_t next = buf_load(rin, lane * 4);
     RleCarry cy = {0, 0, 0};
     // Two copies of the chunk loop: streams that fit one window (every batch stream) run without
-    // the window bookkeeping, which would otherwise sit in scalar registers across the hot loop.
+    // the window bookkeeping, which would otherwise sit in scalar registers across the hot loop,
+    // and let the MNP-5 symbols of many chunks gather in syms[] before the FGK loop codes them (a
+    // run-heavy stream yields a few symbols per chunk: one coding pass per buffer instead of per
+    // chunk; grad -c -m encode 3.77 -> 2.89 ms, photo unchanged).
     auto chunks = [&](auto windowed) __attribute__((always_inline)) {
         constexpr bool kWin = decltype(windowed)::value;
-        for (uint32_t ci = 0; ci < nch && !fgk.bad; ++ci, ioff += 256) {
-            prio_by_progress(ci, nch);
-            const uint32_t chunk = next;
-            if constexpr (kWin) {
-                if (ioff >= window) {  // slide the input window up to the next chunk
-                    const uint64_t at = 256ull * (ci + 1);
-                    rin = make_rsrc(bt.in + uni64(bt.in_offs[sid]) + at,
-                                    (uint32_t)min((n - min(n, at) + 3u) & ~3ull, (uint64_t)kMaxBufBytes));
-                    ioff = 0;
+        uint32_t q1 = 0, q2 = 0, q3 = 0;
+        if constexpr (!kWin && HC_ENC_DEEP) {
+            q1 = buf_load(rin, 256 + lane * 4);
+            q2 = buf_load(rin, 512 + lane * 4);
+            q3 = buf_load(rin, 768 + lane * 4);
+            ioff = 1024;
+        }
+        uint32_t np = 0;       // symbols pending in syms[]
+        uint32_t chunk = 0;
+        bool redo = false;     // the chunk did not fit the pending symbols: again, after coding them
+        for (uint32_t ci = 0;;) {
+            const bool more = ci < nch && !fgk.bad;
+            uint32_t full = 0;
+            if (more) {
+                const uint32_t m = ci + 1 < nch ? 256u : (uint32_t)(n - 256ull * ci);
+                if (!redo) {
+                    prio_by_progress(ci, nch);
+                    chunk = next;
+                    if constexpr (kWin) {
+                        if (ioff >= window) {  // slide the input window up to the next chunk
+                            const uint64_t at = 256ull * (ci + 1);
+                            rin = make_rsrc(bt.in + uni64(bt.in_offs[sid]) + at,
+                                            (uint32_t)min((n - min(n, at) + 3u) & ~3ull, (uint64_t)kMaxBufBytes));
+                            ioff = 0;
+                        }
+                        if ((sink.wout - sink.wbase) * 4ull >= window) sink.rebase(bt.out + out_off, cap);
+                        next = buf_load(rin, ioff + lane * 4);  // out of range past the end: reads 0
+                    } else if constexpr (HC_ENC_DEEP) {
+                        next = q1;
+                        q1 = q2;
+                        q2 = q3;
+                        q3 = buf_load(rin, ioff + lane * 4);
+                    } else {
+                        next = buf_load(rin, ioff + lane * 4);
+                    }
+                    ioff += 256;
                 }
-                if ((sink.wout - sink.wbase) * 4ull >= window) sink.rebase(bt.out + out_off, cap);
+                if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
+                    fgk.T.syms[lane] = chunk;
+                    __builtin_amdgcn_wave_barrier();
+                    np = m;
+                    full = 1;  // coded at once
+                } else {
+                    // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel; symbols
+                    // gather in syms[] (windowed streams: coded per chunk)
+                    HC_PROF_BEGIN();
+                    const uint32_t np0 = np;
+                    np = rle_chunk<kSrc>(chunk, m, ci + 1 == nch ? 1u : 0u, cy, sb_w, np, kWin ? 342u : kSymWords * 4,
+                                         fgk.scr32(), lane, full);
+                    HC_PROF_END(4);
+                    if (kWin) {
+                        full = !full;  // code this chunk's symbols now (the chunk itself always fits)
+                        redo = false;
+                    } else {
+                        redo = full != 0;
+                        // code them now, too, when a next chunk like this one would not fit (a
+                        // photo's chunk fills half the buffer: no chunk runs twice)
+                        full |= np + (np - np0) > kSymWords * 4 ? 1u : 0u;
+                    }
+                }
+                if (!redo) ++ci;
             }
-            next = buf_load(rin, ioff + lane * 4);  // out of range past the end: reads 0
-            const uint32_t m = ci + 1 < nch ? 256u : (uint32_t)(n - 256ull * ci);
-            if (kSrc == SRC_SYMBOLS) {  // a ready symbol stream (adaptive path)
-                fgk.T.syms[lane] = chunk;
-                __builtin_amdgcn_wave_barrier();
-                if constexpr (kTab) code_all_tab(m);
-                else code_all(m);
-                nsym += m;
-                continue;
+            if (full || (!more && np)) {  // the serial FGK pass over the pending symbols
+                if constexpr (kTab) code_all_tab(np);
+                else code_all(np);
+                nsym += np;
+                np = 0;
             }
-            // transform.cpp:220-229 (diff) + 241-279 (MNP-5 RLE), lane-parallel, then serial FGK
-            HC_PROF_BEGIN();
-            const uint32_t ns = rle_chunk<kSrc>(chunk, m, ci + 1 == nch ? 1u : 0u, cy, fgk.T.syms,
-                                                fgk.scr32(), lane);
-            HC_PROF_END(4);
-            if constexpr (kTab) code_all_tab(ns);
-            else code_all(ns);
-            nsym += ns;
+            if (!more) break;
         }
     };
     if (n + 512 <= window && cap <= window) chunks(std::false_type{});

@@ -19,7 +19,7 @@ Per byte i of the chunk (c = diffed byte):
 import numpy as np
 
 
-def rle_chunked(data, diff=False, chunk=256):
+def rle_chunked(data, diff=False, chunk=256, fast=False):
     data = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.int64)
     n = data.size
     out = []
@@ -29,6 +29,12 @@ def rle_chunked(data, diff=False, chunk=256):
         m = x.size
         xp = np.concatenate([[prev_x], x[:-1]])
         c = (x - xp) & 255 if diff else x.copy()
+        fin = (base + m == n)
+        if fast and m == chunk and not fin and (c == c_carry).all():
+            sym, R_carry = pure_chunk(R_carry, c_carry)
+            out += list(sym)
+            prev_x = int(x[-1])
+            continue
         cp = np.concatenate([[c_carry], c[:-1]])
         same = (c == cp)
         same[0] = R_carry > 0 and c[0] == c_carry
@@ -53,3 +59,21 @@ def rle_chunked(data, diff=False, chunk=256):
                 out.append(255)
         prev_x, R_carry, c_carry = int(x[-1]), int(R[-1]), int(c[-1])
     return bytes(out)
+
+
+def pure_chunk(R, c):
+    """The encoder's fast path (hc_fgk.hip rle_chunk) for a full, non-final chunk whose 256 diffed
+    bytes all equal the carried byte c: byte i sits at km = (R + i) mod 258, so the chunk emits
+    only the events of the residues 257 (the cut: 255), 0, 1, 2 (c) that fall on i <= 255, in
+    byte order: the cyclic order 257, 0, 1, 2 rotated to start at R when R <= 2 (lane j of the
+    kernel takes entry j). Returns (symbols, run counter after the chunk)."""
+    rot = R + 1 if R <= 2 else 0
+    out = []
+    for j in range(4):
+        q = (j + rot) & 3
+        e = 257 if q == 0 else q - 1
+        i = e + 258 - R
+        i = i - 258 if i >= 258 else i
+        if i <= 255:
+            out.append(255 if e == 257 else c)
+    return bytes(out), (R + 256) % 258

@@ -48,3 +48,22 @@ def test_revert_block_model_random(oracle_mod):
             if diff:
                 want = oracle_mod.undiff(want)
             assert _rb.revert_blocked(sym, diff) == want, (t, diff)
+
+
+
+def test_pure_chunk_fast_path(oracle_mod):
+    """the encoder's fast path for a chunk of 256 copies of the carried byte (rle_chunk_model.
+    pure_chunk) inside the chunked pass equals the reference's FSM, for every run counter R the
+    carry can hold when such a chunk starts (0..257) and both diff settings"""
+    for c in (0, 1, 200):
+        for R in range(258):
+            for diff in (False, True):
+                # stream: filler chunk(s), then a run of c whose counter reaches R at a chunk
+                # edge, then 1-3 pure chunks, then a different byte and a short tail
+                body = bytes([c]) * (R if R else 258)
+                head = bytes([(c + 7) & 255]) * ((-len(body)) % 256 or 256)
+                raw = head + body + bytes([c]) * (256 * (1 + R % 3)) + bytes([(c + 9) & 255, c, c])
+                if diff:  # a stream whose diff is raw (prefix sums)
+                    raw = np.cumsum(np.frombuffer(raw, dtype=np.uint8), dtype=np.uint64).astype(np.uint8).tobytes()
+                want = oracle_mod.rle(oracle_mod.diff(raw) if diff else raw)
+                assert rle_chunked(raw, diff, fast=True) == want, (c, R, diff)
