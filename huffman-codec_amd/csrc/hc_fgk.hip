@@ -162,6 +162,10 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 // 1: non-windowed streams keep four input chunks in flight instead of one. Measured (A/B, C5 -c
 // -m / grad): encode 513 / 2.85 ms against 508 / 2.89 ms with one; the three extra registers live
 // across the FGK loop cost more than the latency they hide.
+// 1: path-cache streams (narrow and wide layouts) code cached symbols six at a time (code_all_batch)
+#ifndef HC_ENC_BATCH
+#define HC_ENC_BATCH 1
+#endif
 #ifndef HC_ENC_DEEP
 #define HC_ENC_DEEP 0
 #endif
@@ -1247,6 +1251,104 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         }
     };
 
+    // Batched hot path (path-cache mode, narrow and wide layouts, HC_ENC_BATCH; model:
+    // tests/fgk_batch_model.py).
+    // Between swaps and splits the tree's shape is fixed and an update only adds 1 to the
+    // weights on the symbol's root path, so the updates of consecutive cached symbols commute:
+    // symbol j of a batch sees the weights before the batch plus one per earlier batch symbol
+    // whose path holds the position. Six symbols at a time, lane 10 j + l taking level l of
+    // symbol j's cached path (level d = its depth: the root, counted once; l > d: root padding):
+    //  1. each lane ORs bit 10 + j into the body word of its position (encoder bodies use bits
+    //     0..9 only; two positions share a word, the odd one in the high half), so the bits of
+    //     body[p] and body[p + 1] tell how many earlier batch symbols pass p and p + 1;
+    //  2. the leader test of every (symbol, level) at once on those weights -- exactly the
+    //     one-symbol loop's update_fast test, symbol by symbol, without stores in between;
+    //  3. the first symbol with a failed level (or no cached path) ends the batch: the bits are
+    //     cleared, the symbols before it commit (one LDS add per path position: +1024 to the
+    //     narrow weight word, +1 to a wide weight, the root once per symbol) and their code
+    //     records go to the sink;
+    //     the failing symbol is coded alone (miss / update_path: walk).
+    // Per symbol ~10 instructions where the one-symbol loop takes ~26, and one dependent chain of
+    // LDS round trips per batch instead of per symbol.
+    constexpr uint32_t kBatch = 6, kLv = 10;
+    static_assert(kInsertDepth + 1 <= kLv && kBatch * kLv <= 64, "batch lanes");
+    auto code_all_batch = [&](uint32_t ns) __attribute__((always_inline)) {
+        const uint32_t bj = lane < kBatch * kLv ? lane / kLv : 7u;  // the lane's symbol (7: idle)
+        const uint32_t bl = lane < kBatch * kLv ? lane % kLv : 0u;  // ... and level
+        const uint32_t bbit = 1024u << bj;                          // its membership bit
+        const uint32_t bbelow = (1024u << bj) - 1024u;              // those of the symbols before
+        const uint64_t idle = ~0ull << (kBatch * kLv);
+        const uint32_t rowb = lds_off16(&fgk.T.pc[0]) + 2 * bl - 2 * kRow;  // + 32 e: row e - 1 (e = 0: pc_miss)
+        const uint32_t recb = lds_off16(&fgk.T.pc[0]) + 2 * kSlotDepth - 2 * kRow;
+        const uint32_t wtb = lds_off(&fgk.T.wt[0]);
+        const uint32_t bdb = lds_off16(&fgk.T.body[0]);
+        const uint32_t whb = lds_off16(&fgk.T.where[0]);
+        const uint32_t scb = lds_off(fgk.scr32());
+        const uint32_t svb = (uint32_t)(size_t)(const lds_u8 *)sb + bj;
+        uint32_t t = 0;
+        while (t < ns) {
+            if (sink.n > 64 - kBatch) sink.pack();
+            const uint32_t jmax = min(kBatch, ns - t);
+            const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + t));
+            const uint32_t e = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv)) >> 10;
+            uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
+            const uint32_t rec = opaque(*(const lds_u16 *)(size_t)(recb + 32 * e));
+            pos = sel(idle, kMissPos, pos);  // idle lanes fail: a failure always exists (fl <= 60)
+            const uint32_t prev = wave_shr1(pos, 0u);  // (across rows: groups of 10 lanes straddle them)
+            const bool real = pos < kRoot;
+            const bool root1 = pos == kRoot && prev != kRoot && bl != 0;  // the path's root lane
+            // 1. membership bits
+            const uint32_t mval = bbit << ((pos & 1u) << 4);
+            const uint32_t ba = real ? bdb + 2 * (pos & ~1u) : scb;
+            __hip_atomic_fetch_or((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)ba, mval,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            // 2. the tests
+            const uint32_t wa = wtb + 4 * pos;
+            const uint32_t w0 = *(const lds_u32 *)(size_t)wa, w1 = *(const lds_u32 *)(size_t)(wa + 4);
+            // (kMissPos reads the zero bodies above the root: no counts, and its weights fail)
+            const uint32_t bpos = min(pos, kRoot + 1);
+            const uint32_t m0 = opaque(*(const lds_u16 *)(size_t)(bdb + 2 * bpos));
+            const uint32_t m1 = opaque(*(const lds_u16 *)(size_t)(bdb + 2 * bpos + 2));
+            const uint32_t c0 = __builtin_popcount(m0 & bbelow), c1 = __builtin_popcount(m1 & bbelow);
+            // update_fast's test: narrow words (weight << 10 | parent) fail below w0 + 1024, wide
+            // weights at or below w0
+            constexpr uint32_t kSh = kW ? 0u : 10u;
+            const uint32_t v0 = w0 + (c0 << kSh), v1 = w1 + (c1 << kSh);
+            const uint64_t fm = ballot(kW ? v1 <= v0 : v1 < v0 + 1024u);
+            const uint32_t jf = min((ff1(fm) * 205u) >> 11, jmax);  // the failing lane / 10
+            // 3. clear, commit, records
+            __hip_atomic_fetch_and((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)ba, ~mval,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const bool add = (real || root1) && bj < jf;
+            __hip_atomic_fetch_add((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)(add ? wa : scb),
+                                   kW ? 1u : 1024u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
+            const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)__umul24(q, kLv * 4), (int)rec);
+            sink.vrec = q < jf ? r : sink.vrec;
+            __builtin_amdgcn_wave_barrier();
+            sink.n += jf;
+            t += jf;
+            if (jf < jmax) {  // symbol t: not cached, or a level reported: coded alone
+                if (sink.n == 64) sink.pack();
+                const uint32_t sym = uni(sb[t]);
+                const uint32_t ent = uni(fgk.T.where[sym]) >> 10;
+                if (ent == 0) {
+                    HC_PROF_BEGIN();
+                    miss(sym);
+                    HC_PROF_END(1);
+                } else {
+                    HC_PROF_BEGIN();
+                    uint32_t pv;
+                    const uint32_t rc = fgk.pc_use(ent, fgk.pc_lane[ent * kRow], pv);
+                    sink.push(rc);
+                    fgk.update_path(pv);
+                    HC_PROF_END(2);
+                }
+                ++t;
+            }
+        }
+    };
+
     // Table mode (kTab): no path cache. The decoder's level tables (levels 1..8, prefix ->
     // where the walk from the root stops) and pcode[] (position -> the code the tables reached
     // it by) give a symbol's code and whole root path from three reads: where[] -> pcode[] ->
@@ -1462,6 +1564,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             }
             if (full || (!more && np)) {  // the serial FGK pass over the pending symbols
                 if constexpr (kTab) code_all_tab(np);
+                else if constexpr (kW <= 1 && HC_ENC_BATCH) code_all_batch(np);
                 else code_all(np);
                 nsym += np;
                 np = 0;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: encoder variants, C5 / grad / C2 A/B (alternating)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-for r in 1 2; do
+for r in ${ROUNDS:-1 2}; do
 for v in ${VARIANTS:-cur shallow base}; do
   if [ $v = cur ]; then L=huffman-codec_amd/lib/libhcodec.so; else L=abvar/$v/libhcodec.so; fi
   HC_LIB_PATH=$L timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-configs --steps 2 > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }

@@ -1,0 +1,86 @@
+"""Model of the encoder's batched hot path (hc_fgk.hip: code_all_batch), checked against the
+one-symbol kernel update (tests/fgk_cache_model.py: kernel_update) on the slot-form tree.
+
+Between swaps and splits the tree's shape is fixed, and the update of a symbol whose every level
+passes the lane-parallel leader test only adds 1 to the weights on its root path. Such updates
+commute, so a batch of up to BATCH cached symbols is tested at once: symbol j's test at position a
+uses the weights before the batch plus one per earlier batch symbol whose path holds a (c0) or
+a + 1 (c1). The kernel gets c0 / c1 from membership bits it ORs into the positions' body words
+(bit 10 + j); the root carries none (every path ends there, and the root's own test always passes
+on the sentinel above it), so a position whose next one is the root counts none there either:
+an undercount that can only report a level falsely, never pass one that fails. The first symbol
+with a reported level or no cached path ends the batch; the symbols before it commit (+1 on every
+path position, the root once each) and it is coded alone, exactly as the one-symbol loop codes it
+(here: the reference's update, huffman.cpp:95-128, which kernel_update equals:
+tests/test_cache_model.py).
+"""
+from fgk_cache_model import ROOT, PathCache, Tree, _word
+
+BATCH = 6
+
+
+def batch_len(t, paths):
+    """paths: root paths (ROOT last) of up to BATCH cached symbols, None for an uncached one;
+    the kernel's jf: the first symbol that fails, len(paths) if none"""
+    for j, p in enumerate(paths):
+        if p is None:
+            return j
+        for a in p:
+            if a == ROOT:
+                break
+            c0 = sum(1 for q in paths[:j] if a in q)
+            c1 = sum(1 for q in paths[:j] if a + 1 != ROOT and (a + 1) in q)
+            if not _word(t, a + 1) + 1024 * c1 >= _word(t, a) + 1024 * c0 + 1024:
+                return j
+    return len(paths)
+
+
+def encode(symbols, batched):
+    """(codes, tree): every symbol's code bits and the final tree; batched=False is the
+    one-symbol loop, True the batched one"""
+    t = Tree()
+    pc = PathCache()
+    codes = []
+    stats = {"batches": 0, "alone": 0}
+
+    def code_path(pv, fresh, sym):
+        code = [p & 1 for p in reversed(pv)]
+        return code[:-1] + [(sym >> k) & 1 for k in range(7, -1, -1)] if fresh else code
+
+    def alone(sym):
+        fresh = t.where[sym] == 0
+        if fresh:
+            t.split(sym)
+        x = t.where[sym]
+        pv = pc.lookup(sym)
+        if pv is None:
+            pv = t.path(x)
+            pc.insert(sym, pv)
+        codes.append(code_path(pv, fresh, sym))
+        t.update(x)
+        for s, lead in t.swaps:
+            pc.on_swap(s, lead)
+
+    def cached(sym):
+        e = pc.slot.get(sym)
+        return None if e is None or t.where[sym] == 0 else pc.ent[e][1] + [ROOT]
+
+    i, n = 0, len(symbols)
+    while i < n:
+        if not batched:
+            alone(symbols[i])
+            i += 1
+            continue
+        paths = [cached(s) for s in symbols[i:i + BATCH]]
+        jf = batch_len(t, paths)
+        stats["batches"] += 1
+        for p in paths[:jf]:
+            codes.append([a & 1 for a in reversed(p[:-1])])
+            for a in p:
+                t.w[a] += 1
+        i += jf
+        if jf < len(paths):
+            stats["alone"] += 1
+            alone(symbols[i])
+            i += 1
+    return codes, t, stats

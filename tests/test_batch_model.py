@@ -1,0 +1,39 @@
+"""The encoder's batched hot path (tests/fgk_batch_model.py, hc_fgk.hip code_all_batch) codes
+every symbol as the one-symbol loop does and leaves the same tree, on the photo / grad / noise
+streams with and without the diff model and on the deep / skewed alphabets of the GPU tests."""
+import numpy as np
+import pytest
+
+from fgk_batch_model import encode
+
+
+def _streams(oracle_mod):
+    out = []
+    for kind in ("photo", "grad", "noise"):
+        raw = oracle_mod.synth(kind, 3, 160, 120).tobytes()
+        out.append(oracle_mod.rle(oracle_mod.diff(raw)))
+        out.append(oracle_mod.rle(raw))
+    rng = np.random.default_rng(5)
+    zipf = 1.0 / np.arange(1, 257) ** 1.1
+    out.append(rng.choice(256, 20000, p=zipf / zipf.sum()).astype(np.uint8).tobytes())
+    sym, a, b = [], 1, 1
+    for s in range(16):
+        sym += [(s * 37) & 255] * a
+        a, b = b, a + b
+    out.append(rng.permutation(np.array(sym, dtype=np.uint8)).tobytes())
+    out.append(b"\x00\xff" * 3000)
+    return out
+
+
+def test_batched_equals_one_symbol_loop(oracle_mod):
+    total = {"batches": 0, "alone": 0, "n": 0}
+    for k, syms in enumerate(_streams(oracle_mod)):
+        syms = list(syms)
+        c1, t1, _ = encode(syms, batched=False)
+        c2, t2, st = encode(syms, batched=True)
+        assert c1 == c2, k
+        assert t1.w == t2.w and t1.body == t2.body and t1.up == t2.up, k
+        total["batches"] += st["batches"]
+        total["alone"] += st["alone"]
+        total["n"] += len(syms)
+    assert total["batches"] < total["n"]
