@@ -162,9 +162,24 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 // 1: non-windowed streams keep four input chunks in flight instead of one. Measured (A/B, C5 -c
 // -m / grad): encode 513 / 2.85 ms against 508 / 2.89 ms with one; the three extra registers live
 // across the FGK loop cost more than the latency they hide.
-// 1: path-cache streams (narrow and wide layouts) code cached symbols six at a time (code_all_batch)
+// 1: path-cache streams (narrow and wide layouts) code cached symbols six at a time (code_all_batch);
+// HC_BATCH_LV lanes per symbol (10: every cached path fits), HC_BATCH_REC 1: code records from
+// ballots of the positions' parities instead of the cache rows' record words (C5 encode 433 ->
+// 412 ms: two LDS operations fewer per step). Measured and dropped: uncached symbols joining the
+// batch with lane-parallel chased paths, inserted into the cache after the commit (570 ms)
+#ifndef HC_BATCH_LV
+#define HC_BATCH_LV 10
+#endif
+#ifndef HC_BATCH_REC
+#define HC_BATCH_REC 1
+#endif
 #ifndef HC_ENC_BATCH
 #define HC_ENC_BATCH 1
+#endif
+// 1: the decoder's hot loop reads the leaf's body through its lanes' own path positions and a
+// DPP broadcast (no scalar address): C5 decode 504 -> 492 ms
+#ifndef HC_DEC_VBODY
+#define HC_DEC_VBODY 1
 #endif
 #ifndef HC_ENC_DEEP
 #define HC_ENC_DEEP 0
@@ -231,7 +246,7 @@ __device__ __forceinline__ uint32_t lds_off(P *p)
 }
 __device__ __forceinline__ uint32_t lds_off16(uint16_t *p) { return (uint32_t)(size_t)(lds_u16 *)p; }
 // b + 2 a on the scalar unit, one instruction (wave-uniform operands)
-__device__ __forceinline__ uint32_t lshl1_add(uint32_t a, uint32_t b)
+[[maybe_unused]] __device__ __forceinline__ uint32_t lshl1_add(uint32_t a, uint32_t b)
 {
     uint32_t r;
     asm("s_lshl1_add_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
@@ -1270,8 +1285,9 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     //     the failing symbol is coded alone (miss / update_path: walk).
     // Per symbol ~10 instructions where the one-symbol loop takes ~26, and one dependent chain of
     // LDS round trips per batch instead of per symbol.
-    constexpr uint32_t kBatch = 6, kLv = 10;
-    static_assert(kInsertDepth + 1 <= kLv && kBatch * kLv <= 64, "batch lanes");
+    constexpr uint32_t kBatch = 6, kLv = HC_BATCH_LV;
+    static_assert(kBatch * kLv <= 64 && kLv >= 4, "batch lanes");
+    constexpr bool kDeep = kInsertDepth + 1 > kLv;  // cached paths may not fit a group: they fail
     auto code_all_batch = [&](uint32_t ns) __attribute__((always_inline)) {
         const uint32_t bj = lane < kBatch * kLv ? lane / kLv : 7u;  // the lane's symbol (7: idle)
         const uint32_t bl = lane < kBatch * kLv ? lane % kLv : 0u;  // ... and level
@@ -1279,7 +1295,9 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         const uint32_t bbelow = (1024u << bj) - 1024u;              // those of the symbols before
         const uint64_t idle = ~0ull << (kBatch * kLv);
         const uint32_t rowb = lds_off16(&fgk.T.pc[0]) + 2 * bl - 2 * kRow;  // + 32 e: row e - 1 (e = 0: pc_miss)
+#if !HC_BATCH_REC
         const uint32_t recb = lds_off16(&fgk.T.pc[0]) + 2 * kSlotDepth - 2 * kRow;
+#endif
         const uint32_t wtb = lds_off(&fgk.T.wt[0]);
         const uint32_t bdb = lds_off16(&fgk.T.body[0]);
         const uint32_t whb = lds_off16(&fgk.T.where[0]);
@@ -1290,9 +1308,12 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             if (sink.n > 64 - kBatch) sink.pack();
             const uint32_t jmax = min(kBatch, ns - t);
             const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + t));
-            const uint32_t e = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv)) >> 10;
+            const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
+            const uint32_t e = wh >> 10;
             uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
+#if !HC_BATCH_REC
             const uint32_t rec = opaque(*(const lds_u16 *)(size_t)(recb + 32 * e));
+#endif
             pos = sel(idle, kMissPos, pos);  // idle lanes fail: a failure always exists (fl <= 60)
             const uint32_t prev = wave_shr1(pos, 0u);  // (across rows: groups of 10 lanes straddle them)
             const bool real = pos < kRoot;
@@ -1313,9 +1334,11 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             // update_fast's test: narrow words (weight << 10 | parent) fail below w0 + 1024, wide
             // weights at or below w0
             constexpr uint32_t kSh = kW ? 0u : 10u;
-            const uint32_t v0 = w0 + (c0 << kSh), v1 = w1 + (c1 << kSh);
+            const uint32_t v0 = w0 + (c0 << kSh);
+            uint32_t v1 = w1 + (c1 << kSh);
+            if constexpr (kDeep) v1 = bl == kLv - 1 && real ? 0u : v1;  // no root lane: too deep, fails
             const uint64_t fm = ballot(kW ? v1 <= v0 : v1 < v0 + 1024u);
-            const uint32_t jf = min((ff1(fm) * 205u) >> 11, jmax);  // the failing lane / 10
+            const uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
             // 3. clear, commit, records
             __hip_atomic_fetch_and((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)ba, ~mval,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -1323,7 +1346,16 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             __hip_atomic_fetch_add((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)(add ? wa : scb),
                                    kW ? 1u : 1024u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
+#if HC_BATCH_REC
+            // the code record 1 << d | bits (bit k: level k's parity, left = even) from two ballots:
+            // the group's parity bits below its first root lane
+            const uint64_t par = ballot(pos & 1u), rtm = ballot(pos == kRoot);
+            const uint32_t gb = __umul24(q, kLv);
+            const uint32_t d = (uint32_t)__builtin_ctz((uint32_t)(rtm >> gb) | (1u << kLv));
+            const uint32_t r = __builtin_amdgcn_ubfe((uint32_t)(par >> gb), 0, d) | (1u << d);
+#else
             const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)__umul24(q, kLv * 4), (int)rec);
+#endif
             sink.vrec = q < jf ? r : sink.vrec;
             __builtin_amdgcn_wave_barrier();
             sink.n += jf;
@@ -1963,13 +1995,29 @@ struct Dec {
             // both sign bits set, one scalar AND
             int32_t left = (int32_t)(i - i1);
             lds_u8 *so = (lds_u8 *)sbuf + (uint32_t)(i - i0);  // the symbol's byte (LDS address in a VGPR)
+#if HC_DEC_VBODY
+            // Every lane reads the body at its own path position; one row_newbcast DPP move gives
+            // rows 0 its lane 0's (the leaf's), so the read needs no scalar address. Lanes 16 and up
+            // (root padding) read lvl_root instead (kRoot: bit 15 clear, no force) and put their
+            // copy of the symbol byte in the landing row, not the block.
+            const uint32_t vbb = lane < 16 ? bbase : lds_off16(&fgk.T.lvl_root[0]) - 2 * kRoot;
+            so += lane < 16 ? 0 : (uint32_t)((uint8_t *)fgk.T.scratch - sbuf);
+            uint32_t e8;
+#endif
             asm("" : "+v"(so));
             do {
+#if HC_DEC_VBODY
+                e8 = uni(pr);  // the leaf's entry
+                d = e8 >> 10;
+                pv = pr & 1023u;
+                b = (uint32_t)__builtin_amdgcn_mov_dpp((int)opaque(*(const lds_u16 *)(size_t)(vbb + 2 * pv)), 0x150, 0xF, 0xF, false);
+#else
                 const uint32_t e8 = uni(pr);  // the leaf's entry
                 x = e8 & 1023u;
                 d = e8 >> 10;
                 b = opaque(*(const lds_u16 *)(size_t)lshl1_add(x, bbase));
                 pv = pr & 1023u;
+#endif
                 in.win <<= d;
                 in.nwin -= d;  // >= 25
                 uint32_t prn;
@@ -1983,6 +2031,9 @@ struct Dec {
             } while ((int32_t)(k & (uint32_t)left) < 0);
             i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
             if (k == 0xFFFFFFFFu) continue;
+#if HC_DEC_VBODY
+            x = e8 & 1023u;
+#endif
             // symbol i - 1 left the loop: the window stands d bits into its code
             finish_symbol(uni(b), pv, k, uni(d), uni(x), i, i0);
         }

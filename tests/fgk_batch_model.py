@@ -35,9 +35,11 @@ def batch_len(t, paths):
     return len(paths)
 
 
-def encode(symbols, batched):
-    """(codes, tree): every symbol's code bits and the final tree; batched=False is the
-    one-symbol loop, True the batched one"""
+def encode(symbols, batched, misses=False, lanes=10):
+    """(codes, tree, stats): every symbol's code bits and the final tree; batched=False is the
+    one-symbol loop, True the batched one. misses=True (HC_BATCH_MISS): a symbol that has a leaf
+    but no cached path joins the batch with its chased root path (if it fits `lanes` levels with
+    the root) and is inserted into the path cache once committed."""
     t = Tree()
     pc = PathCache()
     codes = []
@@ -63,7 +65,14 @@ def encode(symbols, batched):
 
     def cached(sym):
         e = pc.slot.get(sym)
-        return None if e is None or t.where[sym] == 0 else pc.ent[e][1] + [ROOT]
+        if t.where[sym] == 0:
+            return None
+        if e is None:
+            if not misses:
+                return None
+            p = t.path(t.where[sym]) + [ROOT]
+            return p if len(p) <= lanes else None
+        return pc.ent[e][1] + [ROOT]
 
     i, n = 0, len(symbols)
     while i < n:
@@ -74,10 +83,12 @@ def encode(symbols, batched):
         paths = [cached(s) for s in symbols[i:i + BATCH]]
         jf = batch_len(t, paths)
         stats["batches"] += 1
-        for p in paths[:jf]:
+        for s_, p in zip(symbols[i:i + jf], paths[:jf]):
             codes.append([a & 1 for a in reversed(p[:-1])])
             for a in p:
                 t.w[a] += 1
+            if misses and pc.slot.get(s_) is None:
+                pc.insert(s_, p[:-1])
         i += jf
         if jf < len(paths):
             stats["alone"] += 1

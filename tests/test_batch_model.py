@@ -25,12 +25,13 @@ def _streams(oracle_mod):
     return out
 
 
-def test_batched_equals_one_symbol_loop(oracle_mod):
+@pytest.mark.parametrize("misses", [False, True])
+def test_batched_equals_one_symbol_loop(oracle_mod, misses):
     total = {"batches": 0, "alone": 0, "n": 0}
     for k, syms in enumerate(_streams(oracle_mod)):
         syms = list(syms)
         c1, t1, _ = encode(syms, batched=False)
-        c2, t2, st = encode(syms, batched=True)
+        c2, t2, st = encode(syms, batched=True, misses=misses)
         assert c1 == c2, k
         assert t1.w == t2.w and t1.body == t2.body and t1.up == t2.up, k
         total["batches"] += st["batches"]
