@@ -95,3 +95,70 @@ def encode(symbols, batched, misses=False, lanes=10):
             alone(symbols[i])
             i += 1
     return codes, t, stats
+
+
+# ---- the decoder's batched hot path (hc_fgk.hip: Dec::decode_batch)
+
+DEC_BATCH = 6
+TABLE_DEPTH = 8  # the level tables reach codes of up to 8 bits
+
+
+def decode_batch_len(t, paths):
+    """paths: root paths (ROOT last) of the symbols the level tables decoded in a row, None for
+    one whose entry is not a leaf; the kernel's jf. Every batch symbol's increment is added
+    tentatively, so a position's word after the adds counts all batch symbols through it (c0 at
+    its largest, every one of them counted as earlier) while the next position's word is the one
+    read before (c1 = 0): a level fails when word(a + 1) < word(a) + 1024 * C(a)."""
+    cnt = {}
+    for p in paths:
+        if p is None:
+            break
+        for a in p:
+            cnt[a] = cnt.get(a, 0) + 1
+    for j, p in enumerate(paths):
+        if p is None:
+            return j
+        for a in p:
+            if a != ROOT and _word(t, a + 1) < _word(t, a) + 1024 * cnt[a]:
+                return j
+    return len(paths)
+
+
+def decode(symbols, batched):
+    """(tree, stats): decode the stream of `symbols` (the model knows them; the kernel reads them
+    from the tables) with the one-symbol loop or with batches, returning the final tree. Batch
+    symbols are those whose code is at most TABLE_DEPTH bits and leads to a leaf."""
+    t = Tree()
+    stats = {"batches": 0, "alone": 0}
+
+    def alone(sym):
+        if t.where[sym] == 0:
+            t.split(sym)
+        t.update(t.where[sym])
+
+    i, n = 0, len(symbols)
+    while i < n:
+        if not batched:
+            alone(symbols[i])
+            i += 1
+            continue
+        paths = []
+        for s in symbols[i:i + DEC_BATCH]:
+            x = t.where[s]
+            p = t.path(x) if x else None
+            if p is None or len(p) > TABLE_DEPTH:
+                paths.append(None)
+                break
+            paths.append(p + [ROOT])
+        jf = decode_batch_len(t, paths)
+        assert jf <= batch_len(t, paths + [None])  # never passes what the exact test fails
+        stats["batches"] += 1
+        for p in paths[:jf]:
+            for a in p:
+                t.w[a] += 1
+        i += jf
+        if jf < len(paths):
+            stats["alone"] += 1
+            alone(symbols[i])
+            i += 1
+    return t, stats

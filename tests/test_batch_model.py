@@ -38,3 +38,19 @@ def test_batched_equals_one_symbol_loop(oracle_mod, misses):
         total["alone"] += st["alone"]
         total["n"] += len(syms)
     assert total["batches"] < total["n"]
+
+
+def test_decoder_batches_equal_one_symbol_loop(oracle_mod):
+    """Dec::decode_batch's tentative commit (every batch symbol counted before each level test)
+    leaves the tree of the one-symbol loop and fails no level the exact counts pass"""
+    from fgk_batch_model import decode
+    total = {"batches": 0, "alone": 0, "n": 0}
+    for k, syms in enumerate(_streams(oracle_mod)):
+        syms = list(syms)
+        t1, _ = decode(syms, batched=False)
+        t2, st = decode(syms, batched=True)
+        assert t1.w == t2.w and t1.body == t2.body and t1.up == t2.up, k
+        total["batches"] += st["batches"]
+        total["alone"] += st["alone"]
+        total["n"] += len(syms)
+    assert total["batches"] < total["n"]
