@@ -566,7 +566,7 @@ struct Fgk {
         for (uint32_t r = 0; r < 4; ++r) {
             const uint32_t i = r * 64 + lane;
             const uint32_t p = T.lvl[i] & 1023u;
-            const uint64_t m = ballot(i < 254 && (p == s || p == l));
+            const uint64_t m = (ballot(p == s) | ballot(p == l)) & (r == 3 ? 0x3FFFFFFFFFFFFFFFull : ~0ull);
             if (m) return 31 - __builtin_clz(r * 64 + ff1(m) + 2);
         }
         return 8;
@@ -610,7 +610,7 @@ struct Fgk {
             // partner lane's read (quad_perm [1,0,3,2])
             const uint32_t bo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)((b & kContent) | (bo & (31u << kMarkShift)));
-            if (ballot(lane < 2 && ((b >> kMarkShift) & 31u) == gen)) from = min(from, table_level(s, l) + 1);
+            if (ballot(((b >> kMarkShift) & 31u) == gen) & 3u) from = min(from, table_level(s, l) + 1);
             if (!kDec) *(lane < 2 && !(b & kInner) ? &T.where[b & 255u] : scr16()) = (uint16_t)pos;
         } else {
             *(lane < 2 ? &T.body[pos] : scr16()) = (uint16_t)b;

@@ -23,7 +23,7 @@ ENC = {1: "miss (chase, insert, update, push)", 5: "  of which: chase", 6: "  of
 TAB = {1: "miss (not in the tables)", 6: "  of which: chase", 7: "  of which: update (walk)",
        2: "walk after a failed leader test", 3: "record pack", 4: "MNP-5 chunk pass", 5: "level table rebuild"}
 DEC = {1: "walk after a failed leader test", 2: "long code descent / NYT", 3: "update after descent / NYT",
-       4: "RLE + diff revert", 5: "level table rebuild"}
+       4: "RLE + diff revert", 5: "level table rebuild", 6: "batch step (narrow / wide)"}
 
 
 def report(name, names, tr):
