@@ -184,22 +184,17 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 #ifndef HC_ENC_DEEP
 #define HC_ENC_DEEP 0
 #endif
-// decoder (narrow and wide layouts): HC_DEC_BATCH symbols per step from one lookup chain of the
-// level tables and one tentative commit (Dec::decode_batch; 0: the one-symbol loop only)
+// decoder (narrow and wide layouts): up to HC_DEC_BATCH (<= 7) codes per step from one read of
+// the level tables at every bit offset and one tentative commit (Dec::decode_batch; 0: the
+// one-symbol loop only). Measured, C5 decode: one-symbol loop 490 ms, 6 per step 443, 7 per step
+// 430; eight per step in 8-lane groups (the root's increments apart) 437; a first code of >= 8
+// bits sent to the one-symbol step before the chain (HC_DEC_EXIT8): noise decode 237 -> 198 ms,
+// C5 +0.5 %
 #ifndef HC_DEC_BATCH
 #define HC_DEC_BATCH 7
 #endif
-#ifndef HC_DEC_SOLO
-#define HC_DEC_SOLO 0
-#endif
 #ifndef HC_DEC_EXIT8
 #define HC_DEC_EXIT8 1
-#endif
-#ifndef HC_DEC_G
-#define HC_DEC_G 9
-#endif
-#ifndef HC_DEC_EXITRUN
-#define HC_DEC_EXITRUN 1
 #endif
 constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte chunk, <= 342
                                     // (a byte emits 2 only at a run start that follows a run of
@@ -309,6 +304,16 @@ __device__ __forceinline__ uint64_t below_mask(uint32_t k)
 {
     uint64_t r;
     asm("s_bfm_b64 %0, %1, 0" : "=s"(r) : "s"(k));
+    return r;
+}
+// the lanes of the first j groups of nine, (1 << 9 j) - 1 for j <= 7, on the scalar unit (left to
+// itself the compiler may form 9 j on the VALU where SGPRs are scarce)
+__device__ __forceinline__ uint64_t groups9(uint32_t j)
+{
+    uint32_t n;
+    uint64_t r;
+    asm("s_mul_i32 %0, %1, 9" : "=s"(n) : "s"(j));
+    asm("s_bfm_b64 %0, %1, 0" : "=s"(r) : "s"(n));
     return r;
 }
 // per lane: bit lane of m ? t : f (one v_cndmask on a scalar mask)
@@ -1812,7 +1817,6 @@ struct Dec {
     RevCarry rc;
     uint8_t *sbuf;  // this block's symbols (LDS)
     Idx n;
-    uint32_t solo = 0;  // decode steps left without a batch
     uint64_t pacc = 0;  // HC_PROF regions
 
     __device__ __forceinline__ Dec(Tree<kW, true> &t, uint32_t l) : fgk(t, l), lane(l) {}
@@ -1991,14 +1995,12 @@ struct Dec {
     //  3. the increments of the first failing symbol and the ones after it are taken back. The
     //     symbols before it are decoded; it -- or the first symbol whose entry is not a leaf (a
     //     code longer than the tables, or the NYT) -- goes to the one-symbol step.
-    // Returns 0 when the batch took every symbol the window and the block allowed, otherwise the
-    // symbols the one-symbol loop takes next.
-    __device__ __forceinline__ uint32_t decode_batch(Idx i0, Idx &i, Idx i1)
+    // Returns whether the batch took every symbol the window and the block allowed (otherwise the
+    // one-symbol step takes the next one).
+    __device__ __forceinline__ bool decode_batch(Idx i0, Idx &i, Idx i1)
     {
-        // kG = 9 lanes per symbol (levels 8..0, the root included), or 8 (levels 8..1: eight
-        // symbols fill the wave; the root's increments go in one add of their own)
-        constexpr uint32_t kG = HC_DEC_G, kB = kG == 8 ? 8u : HC_DEC_BATCH;
-        static_assert(kG == 8 || (kG == 9 && kB * kG <= 63), "batch lanes");
+        constexpr uint32_t kG = 9, kB = HC_DEC_BATCH;  // lanes per symbol (levels 8..0), symbols
+        static_assert(kB * kG <= 63, "batch lanes");
         const uint32_t bj = lane < kB * kG ? lane / kG : 7u;  // the lane's symbol (7: idle)
         const uint32_t bl = lane < kB * kG ? lane % kG : 8u;  // its level: 8 - bl
         const uint32_t bsh = 24 + min(bl, 7u);
@@ -2008,30 +2010,33 @@ struct Dec {
         const uint32_t n0 = in.nwin;  // >= 33: symbols 0..3 always fit
         // lane o: the depth of a code that starts o bits into the window (its level-8 entry);
         // the chain of symbol starts then runs on registers: S_j+1 = S_j + depth(S_j). sv lane j:
-        // the bits before symbol j; sg: those of the lane's own symbol.
+        // the bits before symbol j.
         const uint32_t dep = opaque(*(const lds_u16 *)(size_t)(l8 + 2 * (uint32_t)((w0 << lane) >> 56))) >> 10;
 #if HC_DEC_EXIT8
         // a first code of 8 bits or more (most of them on a flat alphabet, e.g. noise, where codes
         // are longer than the tables) goes to the one-symbol step at once
-        if (lane_read(dep, 0) >= 8) return HC_DEC_EXITRUN;
+        if (lane_read(dep, 0) >= 8) return false;
 #endif
-        uint32_t S = 0, sv = 0, sg = 0;
+        uint32_t S = 0, sv = 0;
+        const uint32_t bj4 = bj * 4;
 #pragma unroll
         for (uint32_t j = 0; j < kB; ++j) {
             sv = writelane(sv, S, j);
-            sg = sel(((1ull << kG) - 1) << (kG * j), S, sg);
             S += lane_read(dep, S);
         }
         sv = writelane(sv, S, kB);
+        // each lane's own symbol's start: one permute (measured: C5 decode -5.5 % against a select
+        // per symbol in the chain, 14 VALU instructions per step)
+        const uint32_t sg = (uint32_t)__builtin_amdgcn_ds_bpermute((int)bj4, (int)sv);
         // symbols whose code lies inside the window (lane j + 1: the bits up to symbol j's end)
-        const uint32_t nval = __builtin_popcountll(ballot(lane - 1 < kB && sv <= n0));
+        const uint32_t nval = __builtin_popcountll(ballot(sv <= n0) & (((1ull << kB) - 1) << 1));
         const uint32_t jmax = min(nval, (uint32_t)(i1 - i));
         // every symbol's whole root path at once, each group on its own window
         const uint32_t ent = opaque(*(const lds_u16 *)(size_t)(bvb + (((uint32_t)((w0 << sg) >> 32) >> bsh) << 1)));
         const uint32_t pos = ent & 1023u;
         // the lanes that add: each path position once (the entry stops at the lane's own level),
         // symbols inside the window and the block
-        const bool act = (ent >> 10) == 8 - bl && bj < jmax;
+        const uint64_t actm = ballot((ent >> 10) == 8 - bl) & groups9(jmax);
         constexpr uint32_t kI = kW ? 1u : 1024u;
         const uint32_t wa = lds_off(&fgk.T.wt[0]) + 4 * pos;
         const uint32_t scr = lds_off(fgk.scr32());
@@ -2039,27 +2044,24 @@ struct Dec {
         // entry is no leaf has its increments taken back like a failing one)
         const uint32_t b = opaque(*(const lds_u16 *)(size_t)(lds_off16(&fgk.T.body[0]) + 2 * pos));
         const uint32_t w1 = *(const lds_u32 *)(size_t)(wa + 4);
-        __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)(act ? wa : scr), kI, __ATOMIC_RELAXED,
+        __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(actm, wa, scr), kI, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WAVEFRONT);
         const uint32_t wn = *(const lds_u32 *)(size_t)wa;
-        constexpr uint64_t kLeafLanes = kG == 8 ? 0x0101010101010101ull : 0x0040201008040201ull & ((1ull << (kB * kG)) - 1);
+        constexpr uint64_t kLeafLanes = 0x0040201008040201ull & ((1ull << (kB * kG)) - 1);
         // (ff1 of no lane: 0xFFFFFFFF, above every batch)
         const uint32_t jn = ff1(ballot(b & kNotLeaf) & kLeafLanes) / kG;
-        const uint32_t jf = min(min(ff1(ballot(act && w1 < wn)) / kG, jn), jmax);
+        const uint32_t jf = min(min(ff1(ballot(w1 < wn) & actm) / kG, jn), jmax);
         if (jf < jmax)
-            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)(act && bj >= jf ? wa : scr), 0u - kI,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        if constexpr (kG == 8)
-            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)(lane == 0 ? lds_off(&fgk.T.wt[kRoot]) : scr), jf * kI,
+            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(actm & ~groups9(jf), wa, scr), 0u - kI,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         const uint32_t sb0 = (uint32_t)(size_t)(lds_u8 *)sbuf + (uint32_t)(i - i0);
-        *(lds_u8 *)(size_t)(bl == 0 && bj < jf ? sb0 + bj : scr) = (uint8_t)b;
+        *(lds_u8 *)(size_t)sel(kLeafLanes & groups9(jf), sb0 + bj, scr) = (uint8_t)b;
         __builtin_amdgcn_wave_barrier();
         const uint32_t sj = lane_read(sv, jf);
         in.win = w0 << sj;
         in.nwin = n0 - sj;
         i += jf;
-        return jf == jmax ? 0u : 1u;
+        return jf == jmax;
     }
 #endif
 
@@ -2078,24 +2080,16 @@ struct Dec {
             if (in.nwin <= 32) in.refill();
 #if HC_DEC_BATCH
             // narrow / wide: batches, and the symbol that ends one alone
-            uint32_t one = 0;  // the one-symbol loop takes at most this many symbols (0: any)
-            if constexpr (kW <= 1) {
-                if (solo == 0) {
-                    const Idx ib = i;
-                    HC_PROF_BEGIN();
-                    one = decode_batch(i0, i, i1);
-                    HC_PROF_END(6);
-                    if (one == 0) continue;
-                    // a batch that ended at its first symbol: the next HC_DEC_SOLO steps run the
-                    // one-symbol loop (streams of long codes, e.g. noise, fail most batches)
-                    if (i == ib) solo = HC_DEC_SOLO;
-                    if (in.nwin <= 32) in.refill();
-                } else {
-                    --solo;
-                }
+            constexpr bool kOne = kW <= 1;  // the one-symbol step takes one symbol
+            if constexpr (kOne) {
+                HC_PROF_BEGIN();
+                const bool whole = decode_batch(i0, i, i1);
+                HC_PROF_END(6);
+                if (whole) continue;
+                if (in.nwin <= 32) in.refill();
             }
 #else
-            constexpr uint32_t one = 0;
+            constexpr bool kOne = false;
 #endif
             // Hot loop: a leaf within the tables' reach whose update needs no walk. Once a
             // symbol's depth is known the next symbol's table entry is read, before this
@@ -2122,7 +2116,7 @@ struct Dec {
             uint32_t d, x, b, pv, k;
             // loop while no level failed (k = 0xFFFFFFFF) and symbols are left (left < 0):
             // both sign bits set, one scalar AND (after a batch: one symbol)
-            int32_t left = one ? max((int32_t)(i - i1), -(int32_t)one) : (int32_t)(i - i1);
+            int32_t left = kOne ? -1 : (int32_t)(i - i1);
             lds_u8 *so = (lds_u8 *)sbuf + (uint32_t)(i - i0);  // the symbol's byte (LDS address in a VGPR)
 #if HC_DEC_VBODY
             // Every lane reads the body at its own path position; one row_newbcast DPP move gives
