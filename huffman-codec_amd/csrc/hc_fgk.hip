@@ -196,6 +196,14 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 #ifndef HC_DEC_EXIT8
 #define HC_DEC_EXIT8 1
 #endif
+// walk(): after a swap at a position lighter than this, the parent's level is walked at once
+// instead of chasing back to the known path. Measured (C5 encode / decode, noise encode /
+// decode, ms): never 410 / 397, 206 / 184; always 392 / 381, 218 / 197; below 64: 393 / 381,
+// 211 / 190; below 512: 394 / 382, 214 / 193
+#ifndef HC_WALK_LIGHT
+#define HC_WALK_LIGHT 64
+#endif
+constexpr uint32_t kWalkLight = HC_WALK_LIGHT;
 constexpr uint32_t kSymWords = 88;  // encoder: MNP-5 symbols of one 256-byte chunk, <= 342
                                     // (a byte emits 2 only at a run start that follows a run of
                                     // >= 3, so such bytes are >= 3 apart)
@@ -754,10 +762,15 @@ struct Fgk {
             // lane 0 read position s: its address and word, incremented, are the store's
             Wt *dst = &T.wt[s + lane];
             Wt nv = v + kInc;
+            bool again = false;  // the parent's level is walked too (no chase)
             if ((uint32_t)le & 2u) {  // s+1 weighs the same: find the block leader
                 const uint32_t lead =
                     ~le ? s + (uint32_t)__builtin_ctzll(~le) - 1 : leader_far(s + 64, ws);
                 if (lead != p) {
+                    // a light position that swapped: in the long blocks of equal small weights
+                    // its new parent usually ties as well, and testing it here costs one read
+                    // where the chase back to pv and update_from cost several
+                    again = (kWide ? ws : ws >> 10) < kWalkLight;
                     swap(s, lead, !kDec && (!bounded || (kWide ? ws : ws >> 10) >= pc_lb));
                     // the swap rewrites only parent fields below s and lead, never their own
                     // words, so the pre-swap read still holds lead's word when in range
@@ -771,6 +784,10 @@ struct Fgk {
             }
             *(lane == 0 ? dst : scrw()) = nv;
             __builtin_amdgcn_wave_barrier();
+            if (again && p != kRoot) {
+                s = p;
+                continue;
+            }
             // chase from the parent until a position of pv; lane j of td: the j-th one passed
             uint32_t c = p, n = 0, td = kRoot;
             uint64_t on;
