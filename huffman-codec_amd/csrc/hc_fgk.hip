@@ -163,15 +163,12 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 // -m / grad): encode 513 / 2.85 ms against 508 / 2.89 ms with one; the three extra registers live
 // across the FGK loop cost more than the latency they hide.
 // 1: path-cache streams (narrow and wide layouts) code cached symbols six at a time (code_all_batch);
-// HC_BATCH_LV lanes per symbol (10: every cached path fits), HC_BATCH_REC 1: code records from
-// ballots of the positions' parities instead of the cache rows' record words (C5 encode 433 ->
-// 412 ms: two LDS operations fewer per step). Measured and dropped: uncached symbols joining the
-// batch with lane-parallel chased paths, inserted into the cache after the commit (570 ms)
+// HC_BATCH_LV lanes per symbol (10: every cached path fits). Code records come from ballots of the
+// positions' parities (C5 encode 433 -> 412 ms against reading the cache rows' record words: two
+// LDS operations fewer per step). Measured and dropped: uncached symbols joining the batch with
+// lane-parallel chased paths, inserted into the cache after the commit (570 ms)
 #ifndef HC_BATCH_LV
 #define HC_BATCH_LV 10
-#endif
-#ifndef HC_BATCH_REC
-#define HC_BATCH_REC 1
 #endif
 #ifndef HC_ENC_BATCH
 #define HC_ENC_BATCH 1
@@ -1306,42 +1303,38 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     };
 
     // Batched hot path (path-cache mode, narrow and wide layouts, HC_ENC_BATCH; model:
-    // tests/fgk_batch_model.py).
+    // tests/fgk_batch_model.py, test tests/test_batch_model.py).
     // Between swaps and splits the tree's shape is fixed and an update only adds 1 to the
-    // weights on the symbol's root path, so the updates of consecutive cached symbols commute:
-    // symbol j of a batch sees the weights before the batch plus one per earlier batch symbol
-    // whose path holds the position. Six symbols at a time, lane 10 j + l taking level l of
-    // symbol j's cached path (level d = its depth: the root, counted once; l > d: root padding):
-    //  1. each lane ORs bit 10 + j into the body word of its position (encoder bodies use bits
-    //     0..9 only; two positions share a word, the odd one in the high half), so the bits of
-    //     body[p] and body[p + 1] tell how many earlier batch symbols pass p and p + 1;
-    //  2. the leader test of every (symbol, level) at once on those weights -- exactly the
-    //     one-symbol loop's update_fast test, symbol by symbol, without stores in between;
-    //  3. the first symbol with a failed level (or no cached path) ends the batch: the bits are
-    //     cleared, the symbols before it commit (one LDS add per path position: +1024 to the
-    //     narrow weight word, +1 to a wide weight, the root once per symbol) and their code
-    //     records go to the sink;
-    //     the failing symbol is coded alone (miss / update_path: walk).
+    // weights on the symbol's root path, so the updates of consecutive cached symbols commute.
+    // Six symbols at a time, lane 10 j + l taking level l of symbol j's cached path (level d =
+    // its depth: the root, counted once; l > d: root padding), the decoder's tentative commit
+    // (Dec::decode_batch):
+    //  1. every path position of every batch symbol gets its increment (one LDS add: +1024 to the
+    //     narrow weight word, +1 to a wide weight, the root once per symbol), the words of the
+    //     next positions having been read before;
+    //  2. a level fails when that next word is below the position's word after the adds -- the
+    //     one-symbol loop's update_fast test with every batch symbol through the position counted
+    //     as earlier and none through the next one, so it reports levels falsely at worst (the
+    //     exact counts, from membership bits ORed into the body words, measured 394 ms on C5
+    //     where this takes 371);
+    //  3. the first symbol with a failed level or without a cached path (the miss row's kMissPos;
+    //     idle lanes 60..63 carry it too, so one always exists) ends the batch: its increments and
+    //     those after it are taken back, the code records of the ones before it go to the sink,
+    //     and it is coded alone (miss / update_path: walk).
     // Per symbol ~10 instructions where the one-symbol loop takes ~26, and one dependent chain of
     // LDS round trips per batch instead of per symbol.
     constexpr uint32_t kBatch = 6, kLv = HC_BATCH_LV;
-    static_assert(kBatch * kLv <= 64 && kLv >= 4, "batch lanes");
-    constexpr bool kDeep = kInsertDepth + 1 > kLv;  // cached paths may not fit a group: they fail
+    static_assert(kBatch * kLv <= 64 && kLv > kInsertDepth, "batch lanes: every cached path and its root");
     auto code_all_batch = [&](uint32_t ns) __attribute__((always_inline)) {
         const uint32_t bj = lane < kBatch * kLv ? lane / kLv : 7u;  // the lane's symbol (7: idle)
         const uint32_t bl = lane < kBatch * kLv ? lane % kLv : 0u;  // ... and level
-        const uint32_t bbit = 1024u << bj;                          // its membership bit
-        const uint32_t bbelow = (1024u << bj) - 1024u;              // those of the symbols before
         const uint64_t idle = ~0ull << (kBatch * kLv);
         const uint32_t rowb = lds_off16(&fgk.T.pc[0]) + 2 * bl - 2 * kRow;  // + 32 e: row e - 1 (e = 0: pc_miss)
-#if !HC_BATCH_REC
-        const uint32_t recb = lds_off16(&fgk.T.pc[0]) + 2 * kSlotDepth - 2 * kRow;
-#endif
         const uint32_t wtb = lds_off(&fgk.T.wt[0]);
-        const uint32_t bdb = lds_off16(&fgk.T.body[0]);
         const uint32_t whb = lds_off16(&fgk.T.where[0]);
         const uint32_t scb = lds_off(fgk.scr32());
         const uint32_t svb = (uint32_t)(size_t)(const lds_u8 *)sb + bj;
+        const uint32_t l10 = lane * kLv;
         uint32_t t = 0;
         while (t < ns) {
             if (sink.n > 64 - kBatch) sink.pack();
@@ -1350,51 +1343,30 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
             const uint32_t e = wh >> 10;
             uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
-#if !HC_BATCH_REC
-            const uint32_t rec = opaque(*(const lds_u16 *)(size_t)(recb + 32 * e));
-#endif
             pos = sel(idle, kMissPos, pos);  // idle lanes fail: a failure always exists (fl <= 60)
             const uint32_t prev = wave_shr1(pos, 0u);  // (across rows: groups of 10 lanes straddle them)
             const bool real = pos < kRoot;
             const bool root1 = pos == kRoot && prev != kRoot && bl != 0;  // the path's root lane
-            // 1. membership bits
-            const uint32_t mval = bbit << ((pos & 1u) << 4);
-            const uint32_t ba = real ? bdb + 2 * (pos & ~1u) : scb;
-            __hip_atomic_fetch_or((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)ba, mval,
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            // 2. the tests
+            // 1. tentative increments (each path position once, the root once per symbol)
             const uint32_t wa = wtb + 4 * pos;
-            const uint32_t w0 = *(const lds_u32 *)(size_t)wa, w1 = *(const lds_u32 *)(size_t)(wa + 4);
-            // (kMissPos reads the zero bodies above the root: no counts, and its weights fail)
-            const uint32_t bpos = min(pos, kRoot + 1);
-            const uint32_t m0 = opaque(*(const lds_u16 *)(size_t)(bdb + 2 * bpos));
-            const uint32_t m1 = opaque(*(const lds_u16 *)(size_t)(bdb + 2 * bpos + 2));
-            const uint32_t c0 = __builtin_popcount(m0 & bbelow), c1 = __builtin_popcount(m1 & bbelow);
-            // update_fast's test: narrow words (weight << 10 | parent) fail below w0 + 1024, wide
-            // weights at or below w0
-            constexpr uint32_t kSh = kW ? 0u : 10u;
-            const uint32_t v0 = w0 + (c0 << kSh);
-            uint32_t v1 = w1 + (c1 << kSh);
-            if constexpr (kDeep) v1 = bl == kLv - 1 && real ? 0u : v1;  // no root lane: too deep, fails
-            const uint64_t fm = ballot(kW ? v1 <= v0 : v1 < v0 + 1024u);
+            const uint64_t am = ballot(real || root1) & below_mask(kLv * jmax);
+            const uint32_t w1 = *(const lds_u32 *)(size_t)(wa + 4);
+            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am, wa, scb), kW ? 1u : 1024u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const uint32_t wn = *(const lds_u32 *)(size_t)wa;
+            // 2. the tests; 3. the increments from the first failing symbol on taken back
+            const uint64_t fm = (ballot(w1 < wn) & am) | ballot(pos == kMissPos);
             const uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
-            // 3. clear, commit, records
-            __hip_atomic_fetch_and((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)ba, ~mval,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            const bool add = (real || root1) && bj < jf;
-            __hip_atomic_fetch_add((uint32_t *)(__attribute__((address_space(3))) uint32_t *)(size_t)(add ? wa : scb),
-                                   kW ? 1u : 1024u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            if (jf < jmax)
+                __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~below_mask(kLv * jf), wa, scb),
+                                       kW ? 0xFFFFFFFFu : 0xFFFFFC00u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
-#if HC_BATCH_REC
             // the code record 1 << d | bits (bit k: level k's parity, left = even) from two ballots:
             // the group's parity bits below its first root lane
             const uint64_t par = ballot(pos & 1u), rtm = ballot(pos == kRoot);
-            const uint32_t gb = __umul24(q, kLv);
+            const uint32_t gb = l10 - sink.n * kLv;  // q * kLv
             const uint32_t d = (uint32_t)__builtin_ctz((uint32_t)(rtm >> gb) | (1u << kLv));
             const uint32_t r = __builtin_amdgcn_ubfe((uint32_t)(par >> gb), 0, d) | (1u << d);
-#else
-            const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)__umul24(q, kLv * 4), (int)rec);
-#endif
             sink.vrec = q < jf ? r : sink.vrec;
             __builtin_amdgcn_wave_barrier();
             sink.n += jf;

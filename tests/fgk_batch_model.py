@@ -1,18 +1,17 @@
-"""Model of the encoder's batched hot path (hc_fgk.hip: code_all_batch), checked against the
-one-symbol kernel update (tests/fgk_cache_model.py: kernel_update) on the slot-form tree.
+"""Model of the FGK kernels' batched hot paths (hc_fgk.hip: the encoder's code_all_batch, the
+decoder's Dec::decode_batch), checked against the reference's update (huffman.cpp:95-128, which
+the slot-form Tree.update equals: tests/test_cache_model.py).
 
 Between swaps and splits the tree's shape is fixed, and the update of a symbol whose every level
 passes the lane-parallel leader test only adds 1 to the weights on its root path. Such updates
-commute, so a batch of up to BATCH cached symbols is tested at once: symbol j's test at position a
-uses the weights before the batch plus one per earlier batch symbol whose path holds a (c0) or
-a + 1 (c1). The kernel gets c0 / c1 from membership bits it ORs into the positions' body words
-(bit 10 + j); the root carries none (every path ends there, and the root's own test always passes
-on the sentinel above it), so a position whose next one is the root counts none there either:
-an undercount that can only report a level falsely, never pass one that fails. The first symbol
-with a reported level or no cached path ends the batch; the symbols before it commit (+1 on every
-path position, the root once each) and it is coded alone, exactly as the one-symbol loop codes it
-(here: the reference's update, huffman.cpp:95-128, which kernel_update equals:
-tests/test_cache_model.py).
+commute, so a batch of symbols is tested at once. Exactly (batch_len): symbol j's test at position
+a uses the weights before the batch plus one per earlier batch symbol whose path holds a (c0) or
+a + 1 (c1). The kernels test conservatively (tentative_len): every batch symbol's increments are
+added first, so a position's word counts all batch symbols through it (c0 at its largest), and the
+next position's word is the one read before (c1 = 0): a level can be reported falsely, never passed
+when it fails. The first symbol with a reported level (or no cached path / no leaf in the tables)
+ends the batch; the symbols before it commit (+1 on every path position, the root once each) and it
+is coded alone, exactly as the one-symbol loop codes it.
 """
 from fgk_cache_model import ROOT, PathCache, Tree, _word
 
@@ -35,11 +34,12 @@ def batch_len(t, paths):
     return len(paths)
 
 
-def encode(symbols, batched, misses=False, lanes=10):
+def encode(symbols, batched, misses=False, lanes=10, exact=False):
     """(codes, tree, stats): every symbol's code bits and the final tree; batched=False is the
-    one-symbol loop, True the batched one. misses=True (HC_BATCH_MISS): a symbol that has a leaf
-    but no cached path joins the batch with its chased root path (if it fits `lanes` levels with
-    the root) and is inserted into the path cache once committed."""
+    one-symbol loop, True the batched one (the kernel's tentative test; exact=True: exact counts).
+    misses=True (measured and dropped): a symbol that has a leaf but no cached path joins the batch
+    with its chased root path (if it fits `lanes` levels with the root) and is inserted into the
+    path cache once committed."""
     t = Tree()
     pc = PathCache()
     codes = []
@@ -81,7 +81,8 @@ def encode(symbols, batched, misses=False, lanes=10):
             i += 1
             continue
         paths = [cached(s) for s in symbols[i:i + BATCH]]
-        jf = batch_len(t, paths)
+        jf = batch_len(t, paths) if exact else tentative_len(t, paths)
+        assert jf <= batch_len(t, paths)
         stats["batches"] += 1
         for s_, p in zip(symbols[i:i + jf], paths[:jf]):
             codes.append([a & 1 for a in reversed(p[:-1])])
@@ -103,12 +104,12 @@ DEC_BATCH = 6
 TABLE_DEPTH = 8  # the level tables reach codes of up to 8 bits
 
 
-def decode_batch_len(t, paths):
-    """paths: root paths (ROOT last) of the symbols the level tables decoded in a row, None for
-    one whose entry is not a leaf; the kernel's jf. Every batch symbol's increment is added
-    tentatively, so a position's word after the adds counts all batch symbols through it (c0 at
-    its largest, every one of them counted as earlier) while the next position's word is the one
-    read before (c1 = 0): a level fails when word(a + 1) < word(a) + 1024 * C(a)."""
+def tentative_len(t, paths):
+    """paths: root paths (ROOT last) of a batch's symbols, None for one without a cached path (the
+    encoder) or whose table entry is no leaf (the decoder); the kernels' jf. Every batch symbol's
+    increment is added tentatively, so a position's word after the adds counts all batch symbols
+    through it (c0 at its largest, every one of them counted as earlier) while the next position's
+    word is the one read before (c1 = 0): a level fails when word(a + 1) < word(a) + 1024 * C(a)."""
     cnt = {}
     for p in paths:
         if p is None:
@@ -150,7 +151,7 @@ def decode(symbols, batched):
                 paths.append(None)
                 break
             paths.append(p + [ROOT])
-        jf = decode_batch_len(t, paths)
+        jf = tentative_len(t, paths)
         assert jf <= batch_len(t, paths + [None])  # never passes what the exact test fails
         stats["batches"] += 1
         for p in paths[:jf]:

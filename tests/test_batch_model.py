@@ -1,5 +1,5 @@
-"""The encoder's batched hot path (tests/fgk_batch_model.py, hc_fgk.hip code_all_batch) codes
-every symbol as the one-symbol loop does and leaves the same tree, on the photo / grad / noise
+"""The batched hot paths (tests/fgk_batch_model.py; hc_fgk.hip code_all_batch, Dec::decode_batch)
+code every symbol as the one-symbol loop does and leave the same tree, on the photo / grad / noise
 streams with and without the diff model and on the deep / skewed alphabets of the GPU tests."""
 import numpy as np
 import pytest
@@ -25,13 +25,13 @@ def _streams(oracle_mod):
     return out
 
 
-@pytest.mark.parametrize("misses", [False, True])
-def test_batched_equals_one_symbol_loop(oracle_mod, misses):
+@pytest.mark.parametrize("misses,exact", [(False, False), (False, True), (True, True)])
+def test_batched_equals_one_symbol_loop(oracle_mod, misses, exact):
     total = {"batches": 0, "alone": 0, "n": 0}
     for k, syms in enumerate(_streams(oracle_mod)):
         syms = list(syms)
         c1, t1, _ = encode(syms, batched=False)
-        c2, t2, st = encode(syms, batched=True, misses=misses)
+        c2, t2, st = encode(syms, batched=True, misses=misses, exact=exact)
         assert c1 == c2, k
         assert t1.w == t2.w and t1.body == t2.body and t1.up == t2.up, k
         total["batches"] += st["batches"]
