@@ -162,14 +162,11 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 // 1: non-windowed streams keep four input chunks in flight instead of one. Measured (A/B, C5 -c
 // -m / grad): encode 513 / 2.85 ms against 508 / 2.89 ms with one; the three extra registers live
 // across the FGK loop cost more than the latency they hide.
-// 1: path-cache streams (narrow and wide layouts) code cached symbols six at a time (code_all_batch);
-// HC_BATCH_LV lanes per symbol (10: every cached path fits). Code records come from ballots of the
-// positions' parities (C5 encode 433 -> 412 ms against reading the cache rows' record words: two
-// LDS operations fewer per step). Measured and dropped: uncached symbols joining the batch with
-// lane-parallel chased paths, inserted into the cache after the commit (570 ms)
-#ifndef HC_BATCH_LV
-#define HC_BATCH_LV 10
-#endif
+// 1: path-cache streams (narrow and wide layouts) code cached symbols seven at a time
+// (code_all_batch). Code records come from ballots of the positions' parities (C5 encode 433 ->
+// 412 ms against reading the cache rows' record words: two LDS operations fewer per step).
+// Measured and dropped: uncached symbols joining the batch with lane-parallel chased paths,
+// inserted into the cache after the commit (570 ms)
 #ifndef HC_ENC_BATCH
 #define HC_ENC_BATCH 1
 #endif
@@ -1323,8 +1320,12 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     //     and it is coded alone (miss / update_path: walk).
     // Per symbol ~10 instructions where the one-symbol loop takes ~26, and one dependent chain of
     // LDS round trips per batch instead of per symbol.
-    constexpr uint32_t kBatch = 6, kLv = HC_BATCH_LV;
-    static_assert(kBatch * kLv <= 64 && kLv > kInsertDepth, "batch lanes: every cached path and its root");
+    // seven symbols in groups of nine lanes (levels 0..8: every cached path), the root's
+    // increments by lane 63 in the same adds (measured: six symbols in groups of ten, the root in
+    // each group, C5 encode 369 ms against 349)
+    constexpr uint32_t kBatch = 7, kLv = 9;
+    static_assert(kBatch * kLv <= 63 && kLv >= kInsertDepth, "batch lanes: every cached path, lane 63 free");
+    constexpr uint32_t kIncU = kW ? 1u : 1024u;
     auto code_all_batch = [&](uint32_t ns) __attribute__((always_inline)) {
         const uint32_t bj = lane < kBatch * kLv ? lane / kLv : 7u;  // the lane's symbol (7: idle)
         const uint32_t bl = lane < kBatch * kLv ? lane % kLv : 0u;  // ... and level
@@ -1334,7 +1335,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         const uint32_t whb = lds_off16(&fgk.T.where[0]);
         const uint32_t scb = lds_off(fgk.scr32());
         const uint32_t svb = (uint32_t)(size_t)(const lds_u8 *)sb + bj;
-        const uint32_t l10 = lane * kLv;
+        const uint32_t lkl = lane * kLv;
         uint32_t t = 0;
         while (t < ns) {
             if (sink.n > 64 - kBatch) sink.pack();
@@ -1343,28 +1344,30 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
             const uint32_t e = wh >> 10;
             uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
-            pos = sel(idle, kMissPos, pos);  // idle lanes fail: a failure always exists (fl <= 60)
-            const uint32_t prev = wave_shr1(pos, 0u);  // (across rows: groups of 10 lanes straddle them)
-            const bool real = pos < kRoot;
-            const bool root1 = pos == kRoot && prev != kRoot && bl != 0;  // the path's root lane
-            // 1. tentative increments (each path position once, the root once per symbol)
+            // lane 63 (idle) holds the root and adds one increment per batch symbol
+            constexpr uint64_t kL63 = 1ull << 63;
+            pos = sel(idle, kRoot, pos);
             const uint32_t wa = wtb + 4 * pos;
-            const uint64_t am = ballot(real || root1) & below_mask(kLv * jmax);
+            const uint64_t am = (ballot(pos < kRoot) & below_mask(kLv * jmax)) | (jmax ? kL63 : 0);
+            const uint32_t vinc = sel(kL63, jmax * kIncU, kIncU);
+            // 1. tentative increments (each path position once, the root once per symbol)
             const uint32_t w1 = *(const lds_u32 *)(size_t)(wa + 4);
-            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am, wa, scb), kW ? 1u : 1024u, __ATOMIC_RELAXED,
+            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am, wa, scb), vinc, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
             const uint32_t wn = *(const lds_u32 *)(size_t)wa;
             // 2. the tests; 3. the increments from the first failing symbol on taken back
             const uint64_t fm = (ballot(w1 < wn) & am) | ballot(pos == kMissPos);
             const uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
-            if (jf < jmax)
+            if (jf < jmax) {
+                const uint32_t vdec = sel(kL63, (jf - jmax) * kIncU, 0u - kIncU);
                 __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~below_mask(kLv * jf), wa, scb),
-                                       kW ? 0xFFFFFFFFu : 0xFFFFFC00u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                                       vdec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
             const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
             // the code record 1 << d | bits (bit k: level k's parity, left = even) from two ballots:
             // the group's parity bits below its first root lane
             const uint64_t par = ballot(pos & 1u), rtm = ballot(pos == kRoot);
-            const uint32_t gb = l10 - sink.n * kLv;  // q * kLv
+            const uint32_t gb = lkl - sink.n * kLv;  // q * kLv
             const uint32_t d = (uint32_t)__builtin_ctz((uint32_t)(rtm >> gb) | (1u << kLv));
             const uint32_t r = __builtin_amdgcn_ubfe((uint32_t)(par >> gb), 0, d) | (1u << d);
             sink.vrec = q < jf ? r : sink.vrec;

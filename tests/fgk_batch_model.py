@@ -15,7 +15,7 @@ is coded alone, exactly as the one-symbol loop codes it.
 """
 from fgk_cache_model import ROOT, PathCache, Tree, _word
 
-BATCH = 6
+BATCH = 7  # the encoder: seven cached symbols per step (groups of nine lanes)
 
 
 def batch_len(t, paths):
@@ -34,7 +34,7 @@ def batch_len(t, paths):
     return len(paths)
 
 
-def encode(symbols, batched, misses=False, lanes=10, exact=False):
+def encode(symbols, batched, misses=False, lanes=9, exact=False):
     """(codes, tree, stats): every symbol's code bits and the final tree; batched=False is the
     one-symbol loop, True the batched one (the kernel's tentative test; exact=True: exact counts).
     misses=True (measured and dropped): a symbol that has a leaf but no cached path joins the batch
