@@ -190,6 +190,10 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 #ifndef HC_DEC_EXIT8
 #define HC_DEC_EXIT8 1
 #endif
+#ifndef HC_BATCH_YIELD
+#define HC_BATCH_YIELD 5
+#endif
+constexpr uint32_t kBatchYield = HC_BATCH_YIELD;  // Dec::run: twice the symbols per batch worth it
 // walk(): after a swap at a position lighter than this, the parent's level is walked at once
 // instead of chasing back to the known path. Measured (C5 encode / decode, noise encode /
 // decode, ms): never 410 / 397, 206 / 184; always 392 / 381, 218 / 197; below 64: 393 / 381,
@@ -1809,6 +1813,8 @@ struct Dec {
     RevCarry rc;
     uint8_t *sbuf;  // this block's symbols (LDS)
     Idx n;
+    uint32_t bsym = 0, btry = 0;  // this block's batch symbols and batches
+    bool batch_on = true;          // the next block runs batches
     uint64_t pacc = 0;  // HC_PROF regions
 
     __device__ __forceinline__ Dec(Tree<kW, true> &t, uint32_t l) : fgk(t, l), lane(l) {}
@@ -2007,7 +2013,10 @@ struct Dec {
 #if HC_DEC_EXIT8
         // a first code of 8 bits or more (most of them on a flat alphabet, e.g. noise, where codes
         // are longer than the tables) goes to the one-symbol step at once
-        if (lane_read(dep, 0) >= 8) return false;
+        if (lane_read(dep, 0) >= 8) {
+            ++btry;
+            return false;
+        }
 #endif
         uint32_t S = 0, sv = 0;
         const uint32_t bj4 = bj * 4;
@@ -2053,11 +2062,16 @@ struct Dec {
         in.win = w0 << sj;
         in.nwin = n0 - sj;
         i += jf;
+        bsym += jf;
+        ++btry;
         return jf == jmax;
     }
 #endif
 
     // symbols i .. i1 - 1 of the block at i0, one stream
+    // kBat: batches first (narrow / wide layouts), the one-symbol step after each batch that
+    // stops short; otherwise the one-symbol loop alone
+    template <bool kBat = (kW <= 1)>
     __device__ __forceinline__ void decode(Idx i0, Idx &i, Idx i1)
     {
         while (i < i1) {
@@ -2071,8 +2085,8 @@ struct Dec {
             }
             if (in.nwin <= 32) in.refill();
 #if HC_DEC_BATCH
-            // narrow / wide: batches, and the symbol that ends one alone
-            constexpr bool kOne = kW <= 1;  // the one-symbol step takes one symbol
+            // batches, and the symbol that ends one alone (kOne: the one-symbol step takes one)
+            constexpr bool kOne = kBat && kW <= 1;
             if constexpr (kOne) {
                 HC_PROF_BEGIN();
                 const bool whole = decode_batch(i0, i, i1);
@@ -2180,7 +2194,26 @@ struct Dec {
             if (stopped()) break;
             block_start<kWin>(bt, i0);
             const Idx i1 = block_end(i0);
+#if HC_DEC_BATCH
+            // Batches pay where they take several symbols each; on flat alphabets (noise, -c
+            // photos: codes at or past the tables' 8 bits) they stop short and the one-symbol
+            // loop is faster (measured: C4 decode 2.02 s without batches, 3.52 s with them; a
+            // lone wave waits out each batch's table reads). A block runs batches when the last
+            // block that ran them took at least kBatchYield / 2 symbols per batch, and every 8th
+            // block tries them again.
+            if constexpr (kW <= 1) {
+                if (btry) batch_on = 2 * bsym >= kBatchYield * btry;
+                bsym = btry = 0;
+                if (batch_on || ((uint32_t)(i0 >> 8) & 7u) == 0) {
+                    decode<true>(i0, i, i1);
+                    close_block(i0, i1);
+                    continue;
+                }
+            }
+            decode<false>(i0, i, i1);
+#else
             decode(i0, i, i1);
+#endif
             close_block(i0, i1);
         }
     }
