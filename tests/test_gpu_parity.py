@@ -109,6 +109,28 @@ def test_batch_deep_and_skewed(gpu, hc, oracle_mod):
         assert st == [0] * len(raws) and back == raws
 
 
+def test_batch_flat_and_skewed_segments(gpu, hc, oracle_mod):
+    """Streams whose alphabet turns flat and skewed again, segment by segment (noise, photo,
+    grad): the decoder switches its batches off and on per 256-symbol block by their yield (and
+    probes every 8th block), the encoder's batches stop at every uncached symbol; every stream
+    equals the oracle and round-trips"""
+    torch = gpu
+    raws = []
+    for k in range(6):
+        parts = []
+        for j, kind in enumerate(("noise", "photo", "noise", "grad", "photo", "noise")[k % 3:]):
+            parts.append(oracle_mod.synth(kind, 40 + 7 * k + j, 256, 96 + 32 * (j % 3)).tobytes())
+        raws.append(b"".join(parts))
+    for use_diff in (False, True):
+        st, encs, _ = compress_batch(hc, torch, raws, use_diff)
+        assert st == [0] * len(raws)
+        for i, (r, e) in enumerate(zip(raws, encs)):
+            ost, want = oracle_mod.compress(r, use_diff, False, 512)
+            assert ost == 0 and e == want, (i, len(r), use_diff)
+        st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
+        assert st == [0] * len(raws) and back == raws
+
+
 def test_batch_edge_vectors(gpu, hc, vectors):
     torch = gpu
     for mode in ("c", "cm"):
