@@ -1327,7 +1327,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // seven symbols in groups of nine lanes (levels 0..8: every cached path), the root's
     // increments by lane 63 in the same adds (measured: six symbols in groups of ten, the root in
     // each group, C5 encode 369 ms against 349)
-    constexpr uint32_t kBatch = 7, kLv = 9;
+    constexpr uint32_t kBatch = 7, kLv = 9;  // (the masks: groups9)
     static_assert(kBatch * kLv <= 63 && kLv >= kInsertDepth, "batch lanes: every cached path, lane 63 free");
     constexpr uint32_t kIncU = kW ? 1u : 1024u;
     auto code_all_batch = [&](uint32_t ns) __attribute__((always_inline)) {
@@ -1352,7 +1352,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             constexpr uint64_t kL63 = 1ull << 63;
             pos = sel(idle, kRoot, pos);
             const uint32_t wa = wtb + 4 * pos;
-            const uint64_t am = (ballot(pos < kRoot) & below_mask(kLv * jmax)) | (jmax ? kL63 : 0);
+            const uint64_t am = (ballot(pos < kRoot) & groups9(jmax)) | (jmax ? kL63 : 0);
             const uint32_t vinc = sel(kL63, jmax * kIncU, kIncU);
             // 1. tentative increments (each path position once, the root once per symbol)
             const uint32_t w1 = *(const lds_u32 *)(size_t)(wa + 4);
@@ -1364,7 +1364,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             const uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
             if (jf < jmax) {
                 const uint32_t vdec = sel(kL63, (jf - jmax) * kIncU, 0u - kIncU);
-                __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~below_mask(kLv * jf), wa, scb),
+                __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~groups9(jf), wa, scb),
                                        vdec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             }
             const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
