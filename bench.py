@@ -478,6 +478,79 @@ def config_mixed(torch, hc, dev, stream, photos=6144, noises=2048):
     return out, bad
 
 
+CLI_BIN = os.path.join(ROOT, "huffman-codec_amd", "bin", "huffman-codec")
+
+
+def config_cli(reps=7):
+    """C1 (BASELINE configs[0]): the drop-in CLI per file, the reference's own use case (one file
+    per process, main.cpp:152-221): hd01.raw `-c -m` then `-d`, wall clock per process including
+    its start, for this repo's GPU CLI and for the reference binary (oracle/_ref, -O2 and the
+    Makefile's -O0), median of `reps` runs each. hd01.raw is recovered on the box by decoding the
+    reference's committed output tests/golden/corpus/hd01.cm.huf with the reference binary; every
+    binary's .huf must equal that file and every decode must give hd01.raw back. The GPU CLI also
+    reports its in-process phases (HC_CLI_TIMES=1: read, HIP start-up, coding, write), so its wall
+    time splits into process start + library load, HIP start-up and coding."""
+    import statistics
+    import subprocess
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    ref = oracle.REF_BIN_O2 if os.path.exists(oracle.REF_BIN_O2) else oracle.REF_BIN
+    golden = os.path.join(ROOT, "tests", "golden", "corpus", "hd01.cm.huf")
+    if not (os.path.exists(ref) and os.path.exists(CLI_BIN)):
+        return {"what": "C1 hd01 -c -m per file", "skipped": "reference binary or GPU CLI not built"}, 0
+    want = open(golden, "rb").read()
+    tmp = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    bad = 0
+    try:
+        subprocess.run([ref, "-d", "-i", golden, "-o", "hd01.raw"], cwd=tmp, check=True, capture_output=True)
+        raw = open(os.path.join(tmp, "hd01.raw"), "rb").read()
+        out = {"what": "C1: hd01.raw -c -m then -d, one process per file (the reference's use case), "
+                       f"median of {reps} runs, wall clock including process start",
+               "file_bytes": len(raw), "binaries": {}}
+        legs = [("gpu_cli", CLI_BIN), ("reference_O2", oracle.REF_BIN_O2), ("reference_O0", oracle.REF_BIN)]
+        for label, binary in legs:
+            if not os.path.exists(binary):
+                continue
+            env = dict(os.environ, HC_CLI_TIMES="1") if label == "gpu_cli" else None
+            enc_t, dec_t, phases = [], [], {"encode": [], "decode": []}
+            same = rt = True
+            for _ in range(reps):
+                for d, cmd, t in (("encode", ["-c", "-m", "-i", "hd01.raw", "-o", f"{label}.huf"], enc_t),
+                                  ("decode", ["-d", "-i", f"{label}.huf", "-o", f"{label}.out"], dec_t)):
+                    t0 = time.perf_counter()
+                    r = subprocess.run([binary] + cmd, cwd=tmp, capture_output=True, env=env)
+                    t.append(time.perf_counter() - t0)
+                    if r.returncode != 0:
+                        raise RuntimeError(f"C1 {label} {d}: exit {r.returncode}: {r.stderr[-300:]!r}")
+                    for line in r.stderr.decode(errors="replace").splitlines():
+                        if line.startswith("hc-times "):
+                            phases[d].append({k: float(v) for k, v in (f.split("=") for f in line.split()[1:])})
+                same &= open(os.path.join(tmp, f"{label}.huf"), "rb").read() == want
+                rt &= open(os.path.join(tmp, f"{label}.out"), "rb").read() == raw
+            leg = {"binary": os.path.relpath(binary, ROOT), "encode_s": round(statistics.median(enc_t), 4),
+                   "decode_s": round(statistics.median(dec_t), 4), "encode_bytes_identical_to_reference": bool(same),
+                   "round_trip": bool(rt)}
+            for d in ("encode", "decode"):
+                if phases[d]:
+                    med = {k: round(statistics.median(p[k] for p in phases[d]), 3) for k in phases[d][0]}
+                    wall_ms = leg[f"{d}_s"] * 1e3
+                    med["process_start_and_load_ms"] = round(wall_ms - sum(med.values()), 3)
+                    leg[f"{d}_phases_ms"] = med
+            out["binaries"][label] = leg
+            bad += 0 if (same and rt) else 1
+        g, r2 = out["binaries"].get("gpu_cli"), out["binaries"].get("reference_O2")
+        if g and r2:
+            out["gpu_over_reference_O2"] = {"encode": round(g["encode_s"] / r2["encode_s"], 3),
+                                            "decode": round(g["decode_s"] / r2["decode_s"], 3)}
+    finally:
+        for fn in os.listdir(tmp):
+            os.remove(os.path.join(tmp, fn))
+        os.rmdir(tmp)
+    return out, bad
+
+
 def run_configs(torch, hc, dev, stream, only):
     with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
         digests = json.load(f)
@@ -488,6 +561,8 @@ def run_configs(torch, hc, dev, stream, only):
         ("noise", "2048 x 512x512 noise -c -m (worst case: ~262k deep codes per stream)", "noise", 2048, True, 2),
     ]
     res, bad = {}, 0
+    if not only or "C1" in only:
+        res["C1"], bad = config_cli()
     for name, what, kind, S, d, steps in plan:
         if only and name not in only:
             continue
@@ -616,12 +691,15 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dry = args.backend == "gloo"  # the CPU dry run of this same path (StandInBatch per rank)
+    # under torch.distributed.run (LOCAL_WORLD_SIZE set) the process group exists at every world
+    # size, world 1 included: a one-GPU box then runs the RCCL init and collectives of the N-GPU path
+    launched = world > 1 or "LOCAL_WORLD_SIZE" in os.environ
     if dry:
-        if world > 1:
+        if launched:
             dist.init_process_group("gloo")
         dev, stream = torch.device("cpu"), None
     else:
-        if world > 1:
+        if launched:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dev = torch.device("cuda", local)
@@ -640,7 +718,7 @@ def main(argv=None):
     use_diff = not args.no_diff
     N = args.dry_stream_bytes if dry else N_RAW
     b = StandInBatch(torch, rank * S, S, N) if dry else Batch(torch, hc, dev, args.kind, rank * S, S, use_diff)
-    barrier = dist.barrier if world > 1 else None
+    barrier = dist.barrier if dist.is_initialized() else None
     wall, enc_ms, dec_ms = timed(torch, b, stream, args.steps, args.warmup, barrier)
 
     # verification (outside the timed region): every status 0, exact sizes, exact bytes
@@ -678,6 +756,8 @@ def main(argv=None):
                        "backend": "gloo", "bit_exact": None, "fgk_symbols_per_stream": None,
                        "data": "stand-in: pseudo-random bytes per stream (torch generator seeded by the stream index)"})
         result["config"]["workload"] = f"dry run: {args.streams} x {N}-byte streams over {world} rank(s) ({S} per rank)"
+    if dist.is_initialized():
+        result["process_group"] = {"backend": dist.get_backend(), "world": dist.get_world_size()}
     if world == 1 and not dry:
         roof["measured_copy_GBps"] = copy_peak(torch, dev, stream)
     if args.gather:
@@ -708,7 +788,7 @@ def main(argv=None):
             result["configs_bit_exact"] = cbad == 0
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     if cbad:
         raise SystemExit(f"config checks FAILED on {cbad} items")

@@ -3032,7 +3032,8 @@ __global__ __launch_bounds__(64) void par_fix_kernel(DecArgs a, Ws ws)
         uint32_t r = 0, st = 0;  // the exact process before chunk c
         uint64_t o = 0, reruns = 0, c = 0;
         uint64_t dlo = ~0ull, dhi = 0;  // entries written by walks from wrong entries
-        if (nchk == 0) st = HC_ERR_BLOCK_EOF;  // blocks and no block symbols (transform.cpp:170-174)
+        // nchk >= 1: dec_header_kernel sets par only when the stream holds block symbols (an
+        // empty body reaches the serial pass, which reports HC_ERR_BLOCK_EOF, transform.cpp:170-174)
         while (c < nchk && !st) {
             const uint64_t cl = c + lane;
             const bool on = cl < nchk;

@@ -5,9 +5,15 @@
 // aborts exactly like the reference), -o default b.out, the same help text, error messages and
 // exit codes 1-15, and the stderr line "writing N bytes to F". Compression and decompression
 // run on the GPU through include/hcodec.h.
+//
+// HC_CLI_TIMES=1 (bench.py's C1 line): after the normal output, one extra stderr line with the
+// time of each phase inside the process (read, HIP start-up, coding, write, ms), so that the
+// per-file cost can be split from the process start the caller measures around it.
 #include <unistd.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -38,6 +44,11 @@ const char *const kHelp =
 void error_hint(const char *msg)  // main.cpp:147-149
 {
     std::cerr << msg << "try 'huffman-codec -h' for more information\n";
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 }  // namespace
@@ -71,6 +82,10 @@ int main(int argc, char *argv[])
         error_hint("ERROR: invalid 2D data width\n");
         return 4;
     }
+    const char *times_env = std::getenv("HC_CLI_TIMES");
+    const bool times = times_env && times_env[0] == '1';
+    double t_read = 0, t_init = 0, t_code = 0;
+    auto t0 = std::chrono::steady_clock::now();
     std::ifstream ifs(ifp, std::ios::in | std::ios::binary);
     if (ifs.fail()) {
         std::cerr << "ERROR: given input file does not exist\n";
@@ -78,6 +93,13 @@ int main(int argc, char *argv[])
     }
     const std::vector<uint8_t> in((std::istreambuf_iterator<char>(ifs)), std::istreambuf_iterator<char>());
     ifs.close();
+    if (times) {
+        t_read = ms_since(t0);
+        t0 = std::chrono::steady_clock::now();
+        (void)hc_device_ok();  // HIP start-up apart from the coding (otherwise the first call's)
+        t_init = ms_since(t0);
+        t0 = std::chrono::steady_clock::now();
+    }
 
     std::vector<uint8_t> out;
     int st;
@@ -93,6 +115,10 @@ int main(int argc, char *argv[])
         if (st == HC_OK) out.assign(p, p + len);
         hc_free(p);
     }
+    if (times) {
+        t_code = ms_since(t0);
+        t0 = std::chrono::steady_clock::now();
+    }
     if (st != HC_OK) {
         std::cerr << hc_status_message(st);
         return st;
@@ -105,5 +131,10 @@ int main(int argc, char *argv[])
         return 7;
     }
     ofs.write(reinterpret_cast<const char *>(out.data()), (std::streamsize)out.size());
+    if (times) {
+        ofs.close();
+        std::cerr << "hc-times read_ms=" << t_read << " hip_init_ms=" << t_init << " code_ms=" << t_code
+                  << " write_ms=" << ms_since(t0) << "\n";
+    }
     return 0;
 }

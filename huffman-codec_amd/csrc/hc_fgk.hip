@@ -56,19 +56,11 @@ __device__ __forceinline__ uint64_t *trace_buf() { return g_trace; }
 __device__ __forceinline__ uint32_t window_bytes() { return __builtin_amdgcn_readfirstlane(g_window); }
 static uint32_t min_tree() { return g_min_tree; }
 static uint32_t enc_tab() { return g_enc_tab; }
-// 1: narrow streams decode two per wavefront (decode2_kernel), 0: one per wavefront (the default,
-// measured faster: DESIGN.md §3); hc_debug_set_dec_pair, tests run both
-static uint32_t g_dec_pair = 0;
-static uint32_t dec_pair() { return g_dec_pair; }
 #else
 __device__ __forceinline__ uint64_t *trace_buf() { return nullptr; }
 __device__ __forceinline__ uint32_t window_bytes() { return 1u << 30; }
 static uint32_t min_tree() { return 0; }
 static uint32_t enc_tab() { return 0; }
-#ifndef HC_DEC_PAIR
-#define HC_DEC_PAIR 0
-#endif
-static uint32_t dec_pair() { return HC_DEC_PAIR; }
 #endif
 // Streams are addressed through buffer descriptors, whose offsets are 32-bit: each stream's input
 // and output are reached through windows that slide forward by whole multiples of 256 bytes
@@ -159,9 +151,6 @@ constexpr uint32_t kInsertDepth = HC_INSERT_DEPTH;
 // encoder: a miss chases this many levels, then looks the position reached up in the path cache
 constexpr uint32_t kProbe = HC_PROBE;
 constexpr uint32_t kRow = 16;       // u16 per cache entry
-// 1: non-windowed streams keep four input chunks in flight instead of one. Measured (A/B, C5 -c
-// -m / grad): encode 513 / 2.85 ms against 508 / 2.89 ms with one; the three extra registers live
-// across the FGK loop cost more than the latency they hide.
 // 1: path-cache streams (narrow and wide layouts) code cached symbols seven at a time
 // (code_all_batch). Code records come from ballots of the positions' parities (C5 encode 433 ->
 // 412 ms against reading the cache rows' record words: two LDS operations fewer per step).
@@ -169,14 +158,6 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 // inserted into the cache after the commit (570 ms)
 #ifndef HC_ENC_BATCH
 #define HC_ENC_BATCH 1
-#endif
-// 1: the decoder's hot loop reads the leaf's body through its lanes' own path positions and a
-// DPP broadcast (no scalar address): C5 decode 504 -> 492 ms
-#ifndef HC_DEC_VBODY
-#define HC_DEC_VBODY 1
-#endif
-#ifndef HC_ENC_DEEP
-#define HC_ENC_DEEP 0
 #endif
 // decoder (narrow and wide layouts): up to HC_DEC_BATCH (<= 7) codes per step from one read of
 // the level tables at every bit offset and one tentative commit (Dec::decode_batch; 0: the
@@ -263,14 +244,6 @@ __device__ __forceinline__ uint32_t lds_off(P *p)
     return (uint32_t)(size_t)(__attribute__((address_space(3))) P *)p;
 }
 __device__ __forceinline__ uint32_t lds_off16(uint16_t *p) { return (uint32_t)(size_t)(lds_u16 *)p; }
-// b + 2 a on the scalar unit, one instruction (wave-uniform operands)
-[[maybe_unused]] __device__ __forceinline__ uint32_t lshl1_add(uint32_t a, uint32_t b)
-{
-    uint32_t r;
-    asm("s_lshl1_add_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
-    return r;
-}
-
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x)
 {
@@ -394,7 +367,7 @@ struct Fgk {
         // huffman.cpp:23-31: a lone NYT root
         // narrow: sentinels above every weight word; the encoder's last word (above kMissPos)
         // is 0, the decoder's all ones - 1 (see update_fast) but its last 0 too: the pair
-        // (kMissPos, kMissPos + 1) fails every leader test (decode_pair's guard lanes)
+        // (kMissPos, kMissPos + 1) fails every leader test
         for (uint32_t i = lane; i < kWords; i += 64)
             T.wt[i] = i <= kRoot ? (Wt)0 : (kWide ? ~(Wt)0 : (Wt)(i == kWords - 1 && (kDec || !kTabs) ? 0u : (kTabs ? 0xFFFFFFFEu : 0xFFFFFFFFu)));
         if (lane < 2) T.lvl_root[lane] = kRoot;
@@ -1307,7 +1280,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // tests/fgk_batch_model.py, test tests/test_batch_model.py).
     // Between swaps and splits the tree's shape is fixed and an update only adds 1 to the
     // weights on the symbol's root path, so the updates of consecutive cached symbols commute.
-    // Six symbols at a time, lane 10 j + l taking level l of symbol j's cached path (level d =
+    // Seven symbols at a time, lane 9 j + l taking level l of symbol j's cached path (level d =
     // its depth: the root, counted once; l > d: root padding), the decoder's tentative commit
     // (Dec::decode_batch):
     //  1. every path position of every batch symbol gets its increment (one LDS add: +1024 to the
@@ -1318,10 +1291,11 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     //     as earlier and none through the next one, so it reports levels falsely at worst (the
     //     exact counts, from membership bits ORed into the body words, measured 394 ms on C5
     //     where this takes 371);
-    //  3. the first symbol with a failed level or without a cached path (the miss row's kMissPos;
-    //     idle lanes 60..63 carry it too, so one always exists) ends the batch: its increments and
-    //     those after it are taken back, the code records of the ones before it go to the sink,
-    //     and it is coded alone (miss / update_path: walk).
+    //  3. the first symbol with a failed level or without a cached path (the miss row's kMissPos)
+    //     ends the batch: its increments and those after it are taken back, the code records of
+    //     the ones before it go to the sink, and it is coded alone (miss / update_path: walk).
+    //     Without such a symbol (the empty failure mask's ff1 is 0xFFFFFFFF) jf clamps to jmax;
+    //     idle lane 63 holds the root, which never fails.
     // Per symbol ~10 instructions where the one-symbol loop takes ~26, and one dependent chain of
     // LDS round trips per batch instead of per symbol.
     // seven symbols in groups of nine lanes (levels 0..8: every cached path), the root's
@@ -1550,13 +1524,6 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // chunk; grad -c -m encode 3.77 -> 2.89 ms, photo unchanged).
     auto chunks = [&](auto windowed) __attribute__((always_inline)) {
         constexpr bool kWin = decltype(windowed)::value;
-        uint32_t q1 = 0, q2 = 0, q3 = 0;
-        if constexpr (!kWin && HC_ENC_DEEP) {
-            q1 = buf_load(rin, 256 + lane * 4);
-            q2 = buf_load(rin, 512 + lane * 4);
-            q3 = buf_load(rin, 768 + lane * 4);
-            ioff = 1024;
-        }
         uint32_t np = 0;       // symbols pending in syms[]
         uint32_t chunk = 0;
         bool redo = false;     // the chunk did not fit the pending symbols: again, after coding them
@@ -1577,11 +1544,6 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                         }
                         if ((sink.wout - sink.wbase) * 4ull >= window) sink.rebase(bt.out + out_off, cap);
                         next = buf_load(rin, ioff + lane * 4);  // out of range past the end: reads 0
-                    } else if constexpr (HC_ENC_DEEP) {
-                        next = q1;
-                        q1 = q2;
-                        q2 = q3;
-                        q3 = buf_load(rin, ioff + lane * 4);
                     } else {
                         next = buf_load(rin, ioff + lane * 4);
                     }
@@ -1662,13 +1624,6 @@ struct BitSource {
             nxt = buf_load(rs, cbase + 256 + lane * 4);
             ridx = 0;
         }
-    }
-    // the next 32 bits of the stream (decode_pair keeps the window itself)
-    __device__ __forceinline__ uint32_t take()
-    {
-        const uint32_t w = lane_read(chunk, ridx);
-        next_word();
-        return w;
     }
     // push the next 32 bits (needs nwin <= 32)
     __device__ __forceinline__ void refill()
@@ -1797,8 +1752,7 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
 
 // One stream's decoder (huffman.cpp:60-93 + transform.cpp:386-406 per symbol, then the RLE and
 // diff revert of transform.cpp:137-159 / 231-239 per 256-symbol block; header main.cpp:90-104).
-// decode_kernel runs one per wavefront; decode2_kernel runs two per wavefront in its hot loop
-// (decode_pair) and this one-stream code for everything that leaves it.
+// decode_kernel runs one per wavefront.
 template <int kW, int kDst>
 struct Dec {
     // symbol indices: 32-bit below 2^32 symbols (narrow / wide), 64-bit for the huge layout
@@ -2124,29 +2078,19 @@ struct Dec {
             // both sign bits set, one scalar AND (after a batch: one symbol)
             int32_t left = kOne ? -1 : (int32_t)(i - i1);
             lds_u8 *so = (lds_u8 *)sbuf + (uint32_t)(i - i0);  // the symbol's byte (LDS address in a VGPR)
-#if HC_DEC_VBODY
-            // Every lane reads the body at its own path position; one row_newbcast DPP move gives
+            // The leaf's body: every lane reads the body at its own path position; one row_newbcast DPP move gives
             // rows 0 its lane 0's (the leaf's), so the read needs no scalar address. Lanes 16 and up
             // (root padding) read lvl_root instead (kRoot: bit 15 clear, no force) and put their
             // copy of the symbol byte in the landing row, not the block.
             const uint32_t vbb = lane < 16 ? bbase : lds_off16(&fgk.T.lvl_root[0]) - 2 * kRoot;
             so += lane < 16 ? 0 : (uint32_t)((uint8_t *)fgk.T.scratch - sbuf);
             uint32_t e8;
-#endif
             asm("" : "+v"(so));
             do {
-#if HC_DEC_VBODY
                 e8 = uni(pr);  // the leaf's entry
                 d = e8 >> 10;
                 pv = pr & 1023u;
                 b = (uint32_t)__builtin_amdgcn_mov_dpp((int)opaque(*(const lds_u16 *)(size_t)(vbb + 2 * pv)), 0x150, 0xF, 0xF, false);
-#else
-                const uint32_t e8 = uni(pr);  // the leaf's entry
-                x = e8 & 1023u;
-                d = e8 >> 10;
-                b = opaque(*(const lds_u16 *)(size_t)lshl1_add(x, bbase));
-                pv = pr & 1023u;
-#endif
                 in.win <<= d;
                 in.nwin -= d;  // >= 25
                 uint32_t prn;
@@ -2160,9 +2104,7 @@ struct Dec {
             } while ((int32_t)(k & (uint32_t)left) < 0);
             i = i0 + uni((uint32_t)(so - (lds_u8 *)sbuf));
             if (k == 0xFFFFFFFFu) continue;
-#if HC_DEC_VBODY
             x = e8 & 1023u;
-#endif
             // symbol i - 1 left the loop: the window stands d bits into its code
             finish_symbol(uni(b), pv, k, uni(d), uni(x), i, i0);
         }
@@ -2250,181 +2192,6 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     prof_store(sid, t0, dec.pacc + dec.fgk.pacc, lane);
 }
 
-// ---------------------------------------------------------- two streams per wavefront --
-
-// decode_pair: the hot loop of Dec::decode for two narrow streams at once, A on lanes 0-31 and B
-// on lanes 32-63, each half reading its own LDS tree. Everything the one-stream loop keeps in
-// scalar registers per stream (the bit window and its fill, the code's leaf entry and depth) is
-// held per half in vector registers, so that one vector instruction serves both streams; what
-// stays scalar (the symbol count, the two store masks, the loop test) is shared.
-//  * Lane l of a half reads, like lane k = l & 15 of the one-stream loop, level 8 - k's table
-//    entry for the code's 8-bit prefix (k >= 8: the root pad); lanes 16-30 repeat lanes 0-14, so
-//    the leaf's entry sits in lanes 0 and 16 of the half and one row_newbcast DPP move gives it to
-//    every lane. Lanes 0-15 of a half are the one-stream loop's path vector.
-//  * Lane 31 of each half reads a guard pad (the decoder's unused where[]: kMissPos twice) whose
-//    weight pair (all ones - 1, 0) fails every leader test, so each half's failure mask is never
-//    empty: the store masks of both halves are the one 64-bit (fail - (1 | 1 << 32)) & ~fail, and
-//    a real failure is any bit but the two guards.
-//  * Every lane of a half reads the leaf's body (one broadcast address) and folds it into the
-//    test (force: all lanes of the half fail, the first at level 0); lanes 0 / 32 store the
-//    symbol byte.
-// The loop leaves when a real level fails in either half (that half's symbol is finished by
-// Dec::finish_symbol; the other half's symbol is complete) or at the end of the block.
-template <int kDst>
-__device__ __forceinline__ void decode_pair(Dec<0, kDst> &A, Dec<0, kDst> &B, uint32_t i0, uint32_t &i, uint32_t i1)
-{
-    const uint32_t lane = A.lane, hl = lane & 31u, k = lane & 15u;
-    const bool hb = lane >= 32;  // lanes of stream B
-    constexpr uint64_t kGuard = 0x8000000080000000ull;
-    // per-lane LDS bases of the lane's half
-    const uint32_t lvl = hb ? lds_off16(&B.fgk.T.lvl[0]) : lds_off16(&A.fgk.T.lvl[0]);
-    const uint32_t guard = hb ? lds_off16(&B.fgk.T.where[0]) : lds_off16(&A.fgk.T.where[0]);
-    const uint32_t vbody = hb ? lds_off16(&B.fgk.T.body[0]) : lds_off16(&A.fgk.T.body[0]);
-    const uint32_t vwt = hb ? lds_off(&B.fgk.T.wt[0]) : lds_off(&A.fgk.T.wt[0]);
-    const uint32_t vscr = hb ? lds_off(&B.fgk.T.scratch[hl]) : lds_off(&A.fgk.T.scratch[hl]);
-    const uint32_t vsyms = hb ? lds_off(&B.fgk.T.syms[0]) : lds_off(&A.fgk.T.syms[0]);
-    const uint32_t vsh = hl == 31 ? 31u : 24 + min(k, 7u);
-    const uint32_t vbase = hl == 31 ? guard : lvl + 2 * (k < 8 ? (256u >> k) - 2 : 0xFFFFFFFEu);
-    // masks held in scalar registers across the loop (left alone, the compiler rebuilds them
-    // from immediates on every symbol)
-    uint64_t klead = 0x0000000100000001ull, kreal = ~kGuard;
-    asm volatile("" : "+s"(klead), "+s"(kreal));
-    while (i < i1) {
-        if (A.fgk.from < 9) A.fgk.build_levels();
-        if (B.fgk.from < 9) B.fgk.build_levels();
-        if (A.in.nwin <= 32) A.in.refill();
-        if (B.in.nwin <= 32) B.in.refill();
-        // the halves' windows
-        uint64_t vwin = hb ? B.in.win : A.in.win;
-        uint32_t vnwin = hb ? B.in.nwin : A.in.nwin;
-        asm volatile("" : "+v"(vwin), "+v"(vnwin));
-        auto path_read = [&](uint64_t w) __attribute__((always_inline)) {
-            return opaque(*(const lds_u16 *)(size_t)(vbase + ((uint32_t)(w >> 32) >> vsh) * 2));
-        };
-        uint32_t pr = path_read(vwin);
-        uint32_t so = vsyms + (i - i0);  // the symbol's byte in the half's block
-        asm volatile("" : "+v"(so));
-        uint32_t e8, b, pv, kf;
-        uint64_t fail;
-        // loop while no real level failed (kf = 0xFFFFFFFF) and symbols are left (left < 0): both
-        // sign bits set, one scalar AND
-        int32_t left = (int32_t)(i - i1);
-        do {
-            e8 = (uint32_t)__builtin_amdgcn_mov_dpp((int)pr, 0x150, 0xF, 0xF, false);  // row_newbcast:0
-            const uint32_t d = e8 >> 10;
-            pv = pr & 1023u;
-            // the leaf's body, the same address in every lane of the half (a broadcast read)
-            b = opaque(*(const lds_u16 *)(size_t)(vbody + (e8 & 1023u) * 2));
-            const uint32_t wa = vwt + pv * 4;
-            const uint32_t w0 = *(const lds_u32 *)(size_t)wa, w1 = *(const lds_u32 *)(size_t)(wa + 4);
-            vwin <<= d;
-            vnwin -= d;
-            const uint32_t prn = path_read(vwin);  // the next code's
-            const uint32_t nv = w0 + 1024u;
-            // a leaf's body is its symbol; inner / NYT (bit 15): every lane of the half fails
-            const uint32_t force = (uint32_t)__builtin_amdgcn_sbfe((int)b, 15, 1);
-            fail = ballot(w1 < (nv | force));
-            const uint64_t sm = (fail - klead) & ~fail;  // lanes below each half's first failure
-            *(lds_u32 *)(size_t)sel(sm, wa, vscr) = nv;
-            *(lds_u8 *)(size_t)sel(klead, so, vscr) = (uint8_t)b;  // the symbol; rewritten if it leaves
-            ++so;
-            ++left;
-            kf = ff1(fail & kreal);
-            const uint64_t rm = ballot(vnwin <= 32u);
-            if (rm) {  // a half's window needs its next word
-                const uint32_t wa32 = ((uint32_t)rm & 1u) ? A.in.take() : 0u;
-                const uint32_t wb32 = ((uint32_t)(rm >> 32) & 1u) ? B.in.take() : 0u;
-                const uint32_t w = hb ? wb32 : wa32;
-                vwin |= (uint64_t)w << ((32u - vnwin) & 63u);
-                vnwin = sel(rm, vnwin + 32u, vnwin);
-            }
-            pr = prn;
-        } while ((int32_t)(kf & (uint32_t)left) < 0);
-        i = (uint32_t)((int32_t)i1 + left);
-        A.in.win = uni64(vwin);
-        A.in.nwin = uni(vnwin);
-        B.in.win = (uint64_t)lane_read((uint32_t)vwin, 32) | ((uint64_t)lane_read((uint32_t)(vwin >> 32), 32) << 32);
-        B.in.nwin = lane_read(vnwin, 32);
-        const uint64_t real = fail & ~kGuard;
-#ifdef HC_PAIR_PRIO
-        if (real) __builtin_amdgcn_s_setprio(3);
-#endif
-        if ((uint32_t)real) {  // symbol i - 1 of A left the loop
-            const uint32_t pa = lane < 16 ? pv : kRoot;
-            A.finish_symbol(uni(b), pa, ff1(fail), uni(e8) >> 10, uni(e8) & 1023u, i, i0);
-        }
-        if (real >> 32) {  // ... of B: its path moved down to lanes 0-15
-            const uint32_t up = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 32) & 63u) * 4), (int)pv);
-            const uint32_t pb = lane < 16 ? up : kRoot;
-            const uint32_t eb = lane_read(e8, 32);
-            B.finish_symbol(lane_read(b, 32), pb, ff1(fail >> 32), eb >> 10, eb & 1023u, i, i0);
-        }
-#ifdef HC_PAIR_PRIO
-        if (real) prio_by_progress(i0, A.n);
-#endif
-    }
-}
-
-// Two narrow streams per wavefront (4 per SIMD: LDS holds 32 streams per CU either way): while
-// both have symbols, their blocks advance in lockstep through decode_pair (a symbol that leaves
-// the shared loop is finished by its stream alone, so the two stay at the same symbol index and
-// their 256-symbol blocks end together); then the longer one finishes alone (Dec::run). A stream
-// that another tree layout owns, or that fails its header, leaves its partner alone from the start.
-template <int kDst>
-__global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void decode2_kernel(Batch bt)
-{
-    __shared__ Tree<0, true> trees[2 * kWaves];
-    const uint32_t lane = lane_id();
-    const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint32_t sa = 2 * (blockIdx.x * kWaves + wv), sb = sa + 1;
-    if (sa >= bt.n) return;
-    Dec<0, kDst> A(trees[2 * wv], lane), B(trees[2 * wv + 1], lane);
-    const bool on_a = A.open(bt, sa);
-    const bool on_b = sb < bt.n && B.open(bt, sb);
-    uint32_t ia = 0, ib = 0;  // where each stream stands (the block of each is ia & ~255)
-    if (on_a && on_b && A.one_window() && B.one_window()) {
-        // guard pads for decode_pair's lane 31 of each half (the decoder leaves where[] unused)
-        *(lane < 2 ? &A.fgk.T.where[lane] : A.fgk.scr16()) = (uint16_t)kMissPos;
-        *(lane < 2 ? &B.fgk.T.where[lane] : B.fgk.scr16()) = (uint16_t)kMissPos;
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t nc = min(A.n, B.n);
-        uint32_t i = 0;
-        for (uint32_t i0 = 0; i0 < nc; i0 += 256) {
-            if (A.stopped() || B.stopped()) break;
-            A.template block_start<false>(bt, i0);
-            B.template block_start<false>(bt, i0);
-            const uint32_t i1 = min(nc, i0 + 256);
-            decode_pair(A, B, i0, i, i1);
-            if (i1 == A.block_end(i0)) A.close_block(i0, i1);
-            if (i1 == B.block_end(i0)) B.close_block(i0, i1);
-        }
-        ia = ib = i;
-    }
-    // the rest of each stream alone, from a block start or from inside the pair's last block
-    if (on_a) {
-        const uint32_t i0 = ia & ~255u;
-        if (ia > i0 && ia < A.block_end(i0)) {  // finish the pair's last block
-            A.decode(i0, ia, A.block_end(i0));
-            A.close_block(i0, A.block_end(i0));
-            ia = i0 + 256;
-        }
-        if (A.one_window()) A.template run<false>(bt, (ia + 255) & ~255u, (ia + 255) & ~255u);
-        else A.template run<true>(bt, (ia + 255) & ~255u, (ia + 255) & ~255u);
-        A.close(bt);
-    }
-    if (on_b) {
-        const uint32_t i0 = ib & ~255u;
-        if (ib > i0 && ib < B.block_end(i0)) {
-            B.decode(i0, ib, B.block_end(i0));
-            B.close_block(i0, B.block_end(i0));
-            ib = i0 + 256;
-        }
-        if (B.one_window()) B.template run<false>(bt, (ib + 255) & ~255u, (ib + 255) & ~255u);
-        else B.template run<true>(bt, (ib + 255) & ~255u, (ib + 255) & ~255u);
-        B.close(bt);
-    }
-}
-
 }  // namespace
 
 // streams that the table-mode encoder holds resident at once: 6 waves per SIMD (its LDS)
@@ -2461,7 +2228,12 @@ static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipSt
     if (ts != st) {
         const hipError_t e1 = hipEventRecord(join, ts);
         const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, join, 0) : e1;
-        if (e == hipSuccess) e = e2;
+        if (e2 != hipSuccess) {
+            // no join: wait for the side stream here, so that an error return never leaves
+            // library work running unordered against the caller's buffers
+            (void)hipStreamSynchronize(ts);
+            if (e == hipSuccess) e = e2;
+        }
     }
     if (fork) (void)hipEventDestroy(fork);  // (released once the recorded work completes)
     if (join) (void)hipEventDestroy(join);
@@ -2489,16 +2261,12 @@ hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)
     Batch b = b0;
     b.min_tree = min_tree();
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
-    const dim3 grid2((b.n + 2 * kWaves - 1) / (2 * kWaves));
-    const bool pair = dec_pair() != 0;
     if (dst == DST_RAW) {
-        if (pair) decode2_kernel<DST_RAW><<<grid2, block, 0, st>>>(b);
-        else decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_RAW><<<grid, block, 0, st>>>(b);
     } else {
-        if (pair) decode2_kernel<DST_SYMBOLS><<<grid2, block, 0, st>>>(b);
-        else decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
     }
@@ -2527,13 +2295,6 @@ extern "C" int hc_debug_set_enc_tab(uint32_t mode)
 {
     // 0: per stream (sampled alphabet), 1: path cache for every stream, 2: tables for every stream
     hc::g_enc_tab = mode > 2 ? 0 : mode;
-    return 0;
-}
-
-extern "C" int hc_debug_set_dec_pair(uint32_t on)
-{
-    // 1: narrow streams decode two per wavefront, 0: one per wavefront (default)
-    hc::g_dec_pair = on ? 1u : 0u;
     return 0;
 }
 

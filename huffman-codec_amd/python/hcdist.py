@@ -21,14 +21,14 @@ def shard(rank, world, per_rank):
 
 def reduce_counters(values, op="sum", device=None):
     t = torch.as_tensor(values, dtype=torch.float64 if op == "max" else torch.int64, device=device)
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():  # world 1 too: the collective runs (RCCL on a one-GPU box)
         dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return t
 
 
 def gather_sizes(lens):
     """All-gather the per-stream encoded sizes: returns a (world * S,) tensor on every rank."""
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not dist.is_initialized():
         return lens.clone()
     parts = [torch.empty_like(lens) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, lens)
@@ -61,7 +61,7 @@ def gather_encoded(buf, offs, lens):
     rank receives any payload but rank 0, and nothing is padded)."""
     packed = pack(buf, offs, lens)
     sizes = gather_sizes(lens)
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not dist.is_initialized() or dist.get_world_size() == 1:
         return packed, sizes
     world, rank = dist.get_world_size(), dist.get_rank()
     per_rank = sizes.view(world, -1).sum(1).tolist()

@@ -398,16 +398,6 @@ def debug_set_par_min(symbols):
         raise HCodecError(f"hc_debug_set_par_min failed: {rc}")
 
 
-def debug_set_dec_pair(on):
-    """Test hook (debug build only, use_debug_build): narrow streams decode two per wavefront
-    (decode2_kernel: on) or one per wavefront (off, the default and the shipping decoder)."""
-    f = _dbg().hc_debug_set_dec_pair
-    f.argtypes = [ctypes.c_uint32]
-    rc = f(1 if on else 0)
-    if rc:
-        raise HCodecError(f"hc_debug_set_dec_pair failed: {rc}")
-
-
 def debug_set_par_skew(nbytes):
     """Test hook (debug build only, use_debug_build): every odd chunk of the parallel block-boundary
     pass walks from its predicted entry shifted by `nbytes` output bytes (0: off), forcing par_fix's

@@ -84,7 +84,10 @@ void hc_free(void *p);
 
 /* Compress n_streams raw streams: [diff model] -> MNP-5 RLE -> FGK -> header, fused in one
  * kernel (one stream per wavefront). flags: 0 or HC_FLAG_DIFF (adaptive streams: the batched
- * adaptive API below). Capacity per stream: hc_compress_bound(in_len, 0) always suffices. */
+ * adaptive API below). Capacity per stream: hc_compress_bound(in_len, 0) always suffices.
+ * The encoder's two modes (see hc_compress_batch_aux) run one after the other on `stream`
+ * here: a batch mixing skewed and flat alphabets is faster through hc_compress_batch_aux with
+ * a second stream (before round 4 the library ran them on a side stream of its own). */
 int hc_compress_batch(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens,
                       uint32_t n_streams, uint32_t flags, uint8_t *out, const uint64_t *out_offs,
                       const uint64_t *out_caps, uint64_t *out_lens, int32_t *status,

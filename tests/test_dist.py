@@ -97,7 +97,7 @@ def test_pack_single_process():
     assert hcdist.pack(buf, offs, lens).tolist() == [0, 1, 2, 30, 31, 32, 33, 34]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_bench_multi_rank_dry_run(world):
     """bench.py's own multi-rank path (shards, barriers, max-over-ranks timing, counter reduction,
     --gather) end to end under the driver's launcher, on CPU: --backend gloo swaps each rank's GPU
@@ -121,6 +121,8 @@ def test_bench_multi_rank_dry_run(world):
     assert len(lines) == 1, p.stdout
     r = json.loads(lines[0])
     assert r["dry_run"] is True and r["n_gpus"] == world and r["steps"] == 3 and r["warmup"] == 1
+    # the launcher's process group exists at world 1 too (the RCCL path on a one-GPU box)
+    assert r["process_group"] == {"backend": "gloo", "world": world}
     assert r["config"]["streams_total"] == S and r["config"]["streams_per_gpu"] == 2
     assert r["value"] > 0 and r["ms_per_step"] > 0 and r["scaling"] == "strong"
     assert r["bits_per_byte"] == 8.0  # the stand-in copies: encoded = raw bytes

@@ -167,7 +167,9 @@ def test_par_bounds_wrong_entries_repaired(gpu, hc, oracle_mod, skew):
 
 def test_par_bounds_no_block_symbols(gpu, hc, oracle_mod, par_everywhere):
     """blocks announced, no block symbol at all (count == header): the reference exits with 14
-    (transform.cpp:170-174) -- also with the parallel pass's threshold at 0"""
+    (transform.cpp:170-174). With the parallel pass's threshold at 0 such a stream still goes
+    through the serial pass: dec_header_kernel marks a stream parallel only when it holds block
+    symbols, and the serial pass is what reports 14 here."""
     torch = gpu
     W = H = 64
     b = 8
