@@ -115,15 +115,33 @@ __device__ __forceinline__ void prof_store(uint32_t sid, uint64_t t0, uint64_t p
 // SIMD's 8 waves run ahead and the last ones finish long after, on a half-empty SIMD. Waves
 // that are behind (by the share of their stream done: below 1/2, 4/5, 19/20, the rest) take a
 // higher priority instead. Within a band the arbiter goes by age, so the last bands are short.
+// The band is recomputed only when progress reaches the next band edge (one scalar compare per
+// chunk or block; the 64-bit products per call, with their operands spilled, cost ~10 instructions).
 template <class I>  // uint32_t, or uint64_t for the huge layout's symbol counts
-__device__ __forceinline__ void prio_by_progress(I done, I total)
-{
-    const uint64_t d = (uint64_t)done * 20;
-    if (d < 10ull * total) __builtin_amdgcn_s_setprio(3);
-    else if (d < 16ull * total) __builtin_amdgcn_s_setprio(2);
-    else if (d < 19ull * total) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-}
+struct Prio {
+    I next = 0;  // the progress at which the band changes next
+    __device__ __forceinline__ void at(I done, I total)
+    {
+        if (done < next) return;
+        const uint64_t d = (uint64_t)done * 20, t = total;
+        // the band and the first progress past it: ceil(t * k / 20) for k = 10, 16, 19
+        uint64_t k;
+        if (d < 10 * t) {
+            __builtin_amdgcn_s_setprio(3);
+            k = 10;
+        } else if (d < 16 * t) {
+            __builtin_amdgcn_s_setprio(2);
+            k = 16;
+        } else if (d < 19 * t) {
+            __builtin_amdgcn_s_setprio(1);
+            k = 19;
+        } else {
+            __builtin_amdgcn_s_setprio(0);
+            k = 0;
+        }
+        next = k ? (I)((t * k + 19) / 20) : (I)~(I)0;
+    }
+};
 
 constexpr uint32_t kRoot = 512;
 constexpr uint32_t kWords = 576;  // positions 0..512 + sentinels 513..575 (s + 63)
@@ -233,7 +251,6 @@ struct alignas(16) Tree {
     uint16_t pcode[kTab ? 516 : 2];
 };
 
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // a byte in LDS (32-bit address)
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -317,22 +334,40 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t x, uint32_t fill)
     return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x138, 0xF, 0xF, false);
 }
 
-// range-checked view of one stream's bytes; the arguments must be wave-uniform
+// Range-checked view of one stream's bytes: base and size, turned into a buffer descriptor at
+// each access with readfirstlane on every part. The descriptor must be wave-uniform; kept as a
+// value across the loops, the compiler sometimes held it in VGPRs (a u64 min() lowered through
+// f64, or SGPR pressure) and wrapped every load through it in a waterfall loop over lanes (~12
+// instructions and an exec save per chunk). The readfirstlanes fold away when the parts sit in
+// SGPRs, and cost 3 VALU instead of a waterfall when they do not.
+struct rsrc_t {
+    uint64_t base;
+    uint32_t bytes;
+};
 __device__ __forceinline__ rsrc_t make_rsrc(const uint8_t *p, uint32_t bytes)
 {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), (short)0, (int)bytes, 0x00020000);
+    return rsrc_t{(uint64_t)(size_t)p, bytes};
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hw_rsrc(rsrc_t r)
+{
+    // (readfirstlane returns int: each half goes through uint32_t before widening, or a low
+    // word with bit 31 set would sign-extend into the high word)
+    const uint64_t ua = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r.base) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r.base >> 32)) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint8_t *>((size_t)ua), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane(r.bytes), 0x00020000);
 }
 __device__ __forceinline__ uint32_t buf_load(rsrc_t r, uint32_t off)
 {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+    return __builtin_amdgcn_raw_buffer_load_b32(hw_rsrc(r), (int)off, 0, 0);
 }
 __device__ __forceinline__ void buf_store(rsrc_t r, uint32_t off, uint32_t v)
 {
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, hw_rsrc(r), (int)off, 0, 0);
 }
 __device__ __forceinline__ void buf_store8(rsrc_t r, uint32_t off, uint32_t v)
 {
-    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, hw_rsrc(r), (int)off, 0, 0);
 }
 
 // ------------------------------------------------------------------------------ the tree --
@@ -759,16 +794,21 @@ struct Fgk {
                 s = p;
                 continue;
             }
-            // chase from the parent until a position of pv; lane j of td: the j-th one passed
-            uint32_t c = p, n = 0, td = kRoot;
+            // chase from the parent until a position of pv; lane j of td: the j-th one passed. The
+            // climbing position stays in a VGPR (wave-uniform): each level is a compare, a select
+            // into lane n (a scalar bit mask), the parent read and a mask -- no hop through the
+            // scalar unit (with the position in an SGPR the compiler spent ~6 VALU + 11 SALU per
+            // level on copies, readfirstlane and the address)
+            uint32_t c = vreg(p), n = 0, td = kRoot;
             uint64_t on;
+#pragma unroll 1
             while ((on = ballot(pv == c)) == 0) {
-                td = writelane(td, c, n);
-                if (++n > c) {  // parents sit above children: more levels than the position is a bug
+                td = sel(1ull << n, c, td);
+                if (++n >= 63) {  // a valid path is shorter (pv's kRoot lanes end every climb): a bug
                     bad = 1;
                     return;
                 }
-                c = kWide ? uni(T.up[c]) : (uni((uint32_t)T.wt[c]) & 1023u);
+                c = kWide ? (uint32_t)T.up[c] : ((uint32_t)T.wt[c] & 1023u);
             }
             // lane j < n: chased; lane j >= n: pv's lane j - n + m (kRoot past its lane 63)
             const uint32_t src = lane - n + ff1(on);
@@ -1524,6 +1564,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // chunk; grad -c -m encode 3.77 -> 2.89 ms, photo unchanged).
     auto chunks = [&](auto windowed) __attribute__((always_inline)) {
         constexpr bool kWin = decltype(windowed)::value;
+        Prio<uint32_t> prio;
         uint32_t np = 0;       // symbols pending in syms[]
         uint32_t chunk = 0;
         bool redo = false;     // the chunk did not fit the pending symbols: again, after coding them
@@ -1533,7 +1574,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             if (more) {
                 const uint32_t m = ci + 1 < nch ? 256u : (uint32_t)(n - 256ull * ci);
                 if (!redo) {
-                    prio_by_progress(ci, nch);
+                    prio.at(ci, nch);
                     chunk = next;
                     if constexpr (kWin) {
                         if (ioff >= window) {  // slide the input window up to the next chunk
@@ -1768,6 +1809,7 @@ struct Dec {
     uint8_t *sbuf;  // this block's symbols (LDS)
     Idx n;
     uint32_t bsym = 0, btry = 0;  // this block's batch symbols and batches
+    Prio<Idx> prio;
     bool batch_on = true;          // the next block runs batches
     uint64_t pacc = 0;  // HC_PROF regions
 
@@ -1865,7 +1907,7 @@ struct Dec {
                                  obase < cap ? (uint32_t)min(cap - obase, (uint64_t)kMaxBufBytes) : 0u);
             }
         }
-        prio_by_progress(i0, n);
+        prio.at(i0, n);
     }
 
     // symbol i - 1 (of the block at i0) left the hot loop with its leaf entry's position x and
