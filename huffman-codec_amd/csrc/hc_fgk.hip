@@ -189,6 +189,12 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 #ifndef HC_DEC_EXIT8
 #define HC_DEC_EXIT8 1
 #endif
+#ifndef HC_DEC_DOUBLING
+#define HC_DEC_DOUBLING 1
+#endif
+#ifndef HC_DESCENT2
+#define HC_DESCENT2 1
+#endif
 #ifndef HC_BATCH_YIELD
 #define HC_BATCH_YIELD 5
 #endif
@@ -361,6 +367,11 @@ __device__ __forceinline__ uint32_t buf_load(rsrc_t r, uint32_t off)
 {
     return __builtin_amdgcn_raw_buffer_load_b32(hw_rsrc(r), (int)off, 0, 0);
 }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 buf_load4(rsrc_t r, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(hw_rsrc(r), (int)off, 0, 0);
+}
 __device__ __forceinline__ void buf_store(rsrc_t r, uint32_t off, uint32_t v)
 {
     __builtin_amdgcn_raw_buffer_store_b32(v, hw_rsrc(r), (int)off, 0, 0);
@@ -368,6 +379,18 @@ __device__ __forceinline__ void buf_store(rsrc_t r, uint32_t off, uint32_t v)
 __device__ __forceinline__ void buf_store8(rsrc_t r, uint32_t off, uint32_t v)
 {
     __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, hw_rsrc(r), (int)off, 0, 0);
+}
+
+// inclusive prefix sum over the wave (row shifts, then row broadcasts 15 and 31)
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t x)
+{
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false); // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false); // row_bcast:31
+    return x;
 }
 
 // ------------------------------------------------------------------------------ the tree --
@@ -900,7 +923,8 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t b) { return (w 
 // cyclic order 257, 0, 1, 2 rotated to start at R when R <= 2, lane j < 4 taking entry j.
 template <int kSrc>
 __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t fin, RleCarry &cy, uint8_t *sb,
-                                              uint32_t at, uint32_t cap, uint32_t *scr, uint32_t lane, uint32_t &full)
+                                              uint32_t at, uint32_t cap, uint32_t *scr, uint32_t lane, uint32_t &full,
+                                              uint32_t &start_lanes)
 {
     const uint32_t xprev = (x4 << 8) | (wave_shr1(x4, cy.x << 24) >> 24);
     // bytewise x - xprev (mod 256), SWAR
@@ -909,6 +933,7 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
                             : x4;
     uint8_t *sc = reinterpret_cast<uint8_t *>(scr);
     if (m == 256 && !fin && ballot(c4 != cy.c * 0x01010101u) == 0) {
+        start_lanes = cy.R == 0 ? 1u : 0u;
         const uint32_t R = cy.R;
         const uint32_t rot = R <= 2 ? R + 1 : 0;
         const uint32_t q = (lane + rot) & 3u;
@@ -939,7 +964,9 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
         last = start[b] ? i0 + (int)b : last;
     }
     // latest run start in the lanes below (else the carried run, begun at -R)
-    const uint64_t amask = ballot(any != 0) & ((1ull << lane) - 1ull);
+    const uint64_t anyl = ballot(any != 0);
+    start_lanes = (uint32_t)__builtin_popcountll(anyl);
+    const uint64_t amask = anyl & ((1ull << lane) - 1ull);
     const int src = amask ? 63 - __builtin_clzll(amask) : 0;
     const int below = __builtin_amdgcn_ds_bpermute(src * 4, last);
     int ls = amask ? below : -(int)cy.R;
@@ -993,6 +1020,118 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
     return at + total;
 }
 
+// A full, non-final 1 KB block of a run-heavy stream (tests/rle_chunk_model.py: sparse_block,
+// rle_blocked), lane l holding bytes 16 l .. 16 l + 15 in x[0..3] (one 16-byte load). When the
+// block has at most kSparseStarts run starts and at most 63 symbols, it is coded by segments
+// instead of byte by byte: the carried segment [0, p_0) continues the run before the block, and
+// segment j = [p_j, p_j+1) is a new run. A segment emits its start's count (when the run before
+// it reached R' >= 3: R' - 3) and c, then a symbol for every offset whose residue mod 258 is 0, 1,
+// 2 (c) or 257 (255): the t-th of those is 255 when t % 4 == 3. The carried segment's residues
+// start at the carried counter R instead. Lane j < S holds start j (its segment's length and
+// event count), a scan of the counts places the segments, and each symbol's lane finds its
+// segment by a max-scan over markers (one LDS row). Returns the symbols pending after the block,
+// or kDense with nothing written and the carry unchanged (the caller then codes the block as four
+// 256-byte chunks). The caller guarantees room for 63 symbols.
+#ifndef HC_SPARSE
+#define HC_SPARSE 1
+#endif
+constexpr uint32_t kSparseStarts = 16;
+constexpr uint32_t kDense = 0xFFFFFFFFu;
+template <int kSrc>
+__device__ __forceinline__ uint32_t rle_block(const u32x4 x, RleCarry &cy, uint8_t *sb, uint32_t at, uint32_t *row,
+                                              uint32_t lane)
+{
+    // transform.cpp:220-229: the diffed bytes (lane 0's previous byte is the carry's)
+    uint32_t c[4];
+    uint32_t pb = wave_shr1(x[3], cy.x << 24) >> 24;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t xp = (x[k] << 8) | pb;
+        c[k] = kSrc == SRC_RAW_DIFF ? (((x[k] | 0x80808080u) - (xp & 0x7F7F7F7Fu)) ^ ((x[k] ^ ~xp) & 0x80808080u)) : x[k];
+        pb = x[k] >> 24;
+    }
+    // run starts: bit 4 k + b of M for byte b of c[k] (byte 0 of the block also when R = 0: a cut)
+    uint32_t M = 0;
+    pb = wave_shr1(c[3], cy.c << 24) >> 24;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t d = c[k] ^ ((c[k] << 8) | pb);
+        const uint32_t f = ((((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u) >> 7;  // 1 per nonzero byte
+        M |= ((f | (f >> 7) | (f >> 14) | (f >> 21)) & 15u) << (4 * k);
+        pb = c[k] >> 24;
+    }
+    M |= lane == 0 && cy.R == 0 ? 1u : 0u;
+    const uint32_t cnt = (uint32_t)__builtin_popcount(M);
+    const uint32_t incl = wave_scan_add(cnt);
+    const uint32_t S = lane_read(incl, 63);
+    if (S > kSparseStarts) return kDense;
+    // the starts in order: row[r] = position | run byte << 16 (writes past S land on row[63])
+    {
+        uint32_t r = incl - cnt, m = M;
+        while (ballot(m != 0)) {
+            const uint32_t b = (uint32_t)__builtin_ctz(m | 0x10000u);
+            const uint32_t ck = (b & 8u) ? ((b & 4u) ? c[3] : c[2]) : ((b & 4u) ? c[1] : c[0]);
+            row[m ? r : 63u] = (lane * 16 + b) | (((ck >> (8 * (b & 3u))) & 255u) << 16);
+            r += m ? 1u : 0u;
+            m &= m - 1u;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t pw = row[lane];
+    const bool st = lane < S;
+    const uint32_t p = st ? pw & 0xFFFFu : 1024u;
+    const uint32_t cb = (pw >> 16) & 255u;
+    const uint32_t R0 = cy.R;
+    const uint32_t p0 = S ? lane_read(p, 0) : 1024u;
+    // segment j: [p, pn); the run counter before its start: (R0 + p_0) mod 258 for j = 0, the
+    // previous new run's length mod 258 otherwise
+    const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(1024, (int)p, 0x130, 0xF, 0xF, false);  // wave_shl:1
+    const uint32_t pp = wave_shr1(p, 0u);
+    const uint32_t L = pn - p;
+    auto mod258 = [](uint32_t v) {  // v < 1290
+        return v - 258u * ((v * 2033u) >> 19);
+    };
+    const uint32_t Rp = mod258(lane == 0 ? R0 + p : p - pp);
+    const uint32_t hc = Rp >= 3 ? 1u : 0u;  // the start emits a count R' - 3 first
+    const uint32_t qL = (L * 2033u) >> 19;
+    const uint32_t ne = st ? hc + 4 * qL + min(L - 258u * qL, 3u) : 0u;
+    const uint32_t ninc = wave_scan_add(ne);
+    // the carried segment: lane t < 16 tests its t-th candidate (cycle t >> 2, entry t & 3 of 257,
+    // 0, 1, 2 rotated to start at R0)
+    const uint32_t rot = R0 <= 2 ? R0 + 1 : 0u;
+    const uint32_t q = (lane + rot) & 3u;
+    const uint32_t e = q == 0 ? 257u : q - 1u;
+    const uint32_t ic = mod258(e + 258u - R0) + 258u * (lane >> 2);
+    const uint32_t nc = (uint32_t)__builtin_popcountll(ballot(lane < 16 && ic < p0));
+    const uint32_t total = nc + lane_read(ninc, 63);
+    if (total > 63) return kDense;
+    // markers: each start's key (its first symbol's index, count flag and value, run byte) at row
+    // [its index]; an inclusive max-scan gives every symbol lane its segment (0: the carried one)
+    row[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t base = nc + ninc - ne;
+    row[st ? base : 63u] = 0x80000000u | (base << 24) | (hc << 23) | (((Rp - 3u) & 255u) << 8) | cb;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t key = row[lane];
+    key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x111, 0xF, 0xF, false));  // row_shr:1
+    key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x112, 0xF, 0xF, false));  // row_shr:2
+    key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x114, 0xF, 0xF, false));  // row_shr:4
+    key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x118, 0xF, 0xF, false));  // row_shr:8
+    key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    // a start segment's symbol (selects per lane), else the carried segment's
+    const uint32_t u = lane - ((key >> 24) & 63u), kc = (key >> 23) & 1u;
+    const uint32_t vs = kc && u == 0 ? (key >> 8) & 255u : (((u - kc) & 3u) == 3u ? 255u : key & 255u);
+    const uint32_t v = (key >> 31) ? vs : (e == 257 ? 255u : cy.c);
+    *(lane < total ? sb + at + lane : reinterpret_cast<uint8_t *>(row + 63)) = (uint8_t)v;
+    __builtin_amdgcn_wave_barrier();
+    // carries: the block's last raw and diffed byte, the run counter after it
+    cy.x = lane_read(x[3], 63) >> 24;
+    cy.c = lane_read(c[3], 63) >> 24;
+    cy.R = mod258(S ? 1024u - lane_read(p, S - 1) : R0 + 1024u);
+    return at + total;
+}
+
 // ------------------------------------------------------------------------- output stage --
 
 // Code records: the encoder does not shift bits per symbol. Symbol t's code becomes one record
@@ -1014,17 +1153,7 @@ struct RecSink {
     uint32_t nb;      // how many (< 32)
     uint32_t wout;    // its word index
 
-    // inclusive prefix sum over the wave (row shifts, then row broadcasts 15 and 31)
-    static __device__ __forceinline__ uint32_t scan_add(uint32_t x)
-    {
-        x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true);  // row_shr:1
-        x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true);  // row_shr:2
-        x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true);  // row_shr:4
-        x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true);  // row_shr:8
-        x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false); // row_bcast:15
-        x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false); // row_bcast:31
-        return x;
-    }
+    static __device__ __forceinline__ uint32_t scan_add(uint32_t x) { return wave_scan_add(x); }
 
     // append record rec as number n of the group (outside the hot loop)
     __device__ __forceinline__ void push(uint32_t rec)
@@ -1568,10 +1697,39 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         uint32_t np = 0;       // symbols pending in syms[]
         uint32_t chunk = 0;
         bool redo = false;     // the chunk did not fit the pending symbols: again, after coding them
+        // Run-heavy stretches (a 256-byte chunk whose run starts sit in at most kSparseEnter
+        // lanes) switch to 1 KB blocks coded by segments (rle_block; tests/rle_chunk_model.py:
+        // rle_blocked) while the blocks stay sparse and four full chunks remain before the last
+        // one; blk holds the block at ci (one 16-byte load per lane, the next one in flight).
+        constexpr bool kSparseOn = HC_SPARSE && !kWin && kSrc != SRC_SYMBOLS && !kTab;
+        constexpr uint32_t kSparseEnter = 2;
+        bool sparse = false;
+        u32x4 blk = {0u, 0u, 0u, 0u};
         for (uint32_t ci = 0;;) {
             const bool more = ci < nch && !fgk.bad;
             uint32_t full = 0;
-            if (more) {
+            if (kSparseOn && more && sparse) {
+                if (np + 63 > kSymWords * 4) {
+                    full = 1;  // room for a block's symbols first
+                } else {
+                    prio.at(ci, nch);
+                    HC_PROF_BEGIN();
+                    const uint32_t r = rle_block<kSrc>(blk, cy, sb_w, np, fgk.T.scratch, lane);
+                    HC_PROF_END(4);
+                    if (r != kDense) {
+                        np = r;
+                        ci += 4;
+                        full = np + 63 > kSymWords * 4 ? 1u : 0u;
+                    }
+                    if (r != kDense && ci + 4 < nch) {
+                        blk = buf_load4(rin, 256 * ci + 16 * lane);
+                    } else {  // a dense block or the last chunks: 256-byte chunks from ci
+                        sparse = false;
+                        next = buf_load(rin, 256 * ci + lane * 4);
+                        ioff = 256 * ci + 256;
+                    }
+                }
+            } else if (more) {
                 const uint32_t m = ci + 1 < nch ? 256u : (uint32_t)(n - 256ull * ci);
                 if (!redo) {
                     prio.at(ci, nch);
@@ -1600,9 +1758,14 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                     // gather in syms[] (windowed streams: coded per chunk)
                     HC_PROF_BEGIN();
                     const uint32_t np0 = np;
+                    uint32_t slanes = 64;
                     np = rle_chunk<kSrc>(chunk, m, ci + 1 == nch ? 1u : 0u, cy, sb_w, np, kWin ? 342u : kSymWords * 4,
-                                         fgk.scr32(), lane, full);
+                                         fgk.scr32(), lane, full, slanes);
                     HC_PROF_END(4);
+                    if (kSparseOn && !full && slanes <= kSparseEnter && ci + 5 < nch) {
+                        sparse = true;  // the block at ci + 1 (the chunk loaded ahead is dropped)
+                        blk = buf_load4(rin, 256 * (ci + 1) + 16 * lane);
+                    }
                     if (kWin) {
                         full = !full;  // code this chunk's symbols now (the chunk itself always fits)
                         redo = false;
@@ -1934,12 +2097,57 @@ struct Dec {
             if (fgk.stale >= kRefresh) fgk.from = 0;
             // levels 1..8 of the prefix, lane 64 - j <- level j (lane 8 - j of the path read)
             uint32_t pt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 56) & 63u) * 4), (int)pv);
+            // the position and its body stay in VGPRs (wave-uniform): per level the child address,
+            // one read, a select into lane 63 - depth (a scalar bit mask) and the inner test by a
+            // ballot -- no hop through the scalar unit per level (~22 -> ~13 instructions). The
+            // tree is the kernel's own (input bits only choose the child), and the depth bound ends
+            // the walk down on any inconsistency.
+            // The window's bits are taken straight from a copy of it; the refill (and the 63-level
+            // bound) is tested once per level against lim, the depth the bits in the window reach.
+#if HC_DESCENT2
+            const uint32_t bbase = lds_off16(&fgk.T.body[0]);
+            uint32_t xv = vreg(x), bv = vreg(b);
+            if (in.nwin <= 32) in.refill();
+            uint64_t w = in.win;
+            uint32_t d0 = depth, lim = min(depth + in.nwin, 63u);
+#pragma unroll 1
+            for (;;) {
+                uint64_t inner;
+#pragma unroll 1
+                do {
+                    const uint32_t bit = (uint32_t)(w >> 63);
+                    w <<= 1;
+                    xv = ((bv << 1) & 0x1FEu) | bit;  // child pair * 2 + bit
+                    pt = sel(1ull << (63 - depth), xv, pt);
+                    ++depth;
+                    bv = opaque(*(const lds_u16 *)(size_t)(bbase + 2 * xv));
+                    // go on while the body is inner and the window has bits: one compare
+                    // (inner bit > stop) the branch takes as it is
+                    uint32_t stop = (lim - depth - 1u) >> 31;  // depth >= lim (both < 64)
+                    asm("" : "+s"(stop));  // kept an integer (a compare would go through a select)
+                    inner = ballot(((bv >> 8) & 1u) > stop);
+                } while (inner);
+                if (!ballot(bv & kInner) || depth >= 63) break;
+                // the window is used up (rare): its next word
+                in.win = w;
+                in.nwin -= depth - d0;  // 0
+                in.refill();
+                w = in.win;
+                d0 = depth;
+                lim = min(depth + in.nwin, 63u);
+            }
+            in.win = w;
+            in.nwin -= depth - d0;
+            x = uni(xv);
+            b = uni(bv);
+#else
             do {
                 x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
                 pt = lane == 63 - depth ? x : pt;
                 ++depth;
                 b = uni(fgk.T.body[x]);
             } while ((b & kInner) && depth < 63);
+#endif
             if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
             deep = depth > kInsertDepth;
             pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
@@ -2014,19 +2222,38 @@ struct Dec {
             return false;
         }
 #endif
-        uint32_t S = 0, sv = 0;
+        // The chain by pointer doubling instead of seven serial steps (a lane read, a scalar add and
+        // a lane write each): lane o's next start nx = o + depth(o) (clamped to 63, exact below),
+        // nx2 = nx o nx and nx4 = nx2 o nx2 by two permutes, then lane j applies nx, nx2, nx4 by
+        // the bits of j (two more permutes): lane j <= 7 holds S_j. Values >= 63 were clamped, so a
+        // symbol counts as inside the window when its end is <= min(n0, 62).
+        static_assert(kB <= 7, "the doubling covers starts 0..7");
         const uint32_t bj4 = bj * 4;
+#if HC_DEC_DOUBLING
+        const uint32_t nx = min(lane + dep, 63u);
+        const uint32_t nx2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nx * 4), (int)nx);
+        const uint32_t nx4 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nx2 * 4), (int)nx2);
+        uint32_t sv = sel(0xAAAAAAAAAAAAAAAAull, lane_read(nx, 0), 0u);  // lanes with bit 0: S_1
+        const uint32_t s2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sv * 4), (int)nx2);
+        sv = sel(0xCCCCCCCCCCCCCCCCull, s2, sv);
+        const uint32_t s4 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sv * 4), (int)nx4);
+        sv = sel(0xF0F0F0F0F0F0F0F0ull, s4, sv);
+        const uint32_t vlim = min(n0, 62u);
+#else
+        uint32_t S = 0, sv = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kB; ++j) {
             sv = writelane(sv, S, j);
             S += lane_read(dep, S);
         }
         sv = writelane(sv, S, kB);
+        const uint32_t vlim = n0;
+#endif
         // each lane's own symbol's start: one permute (measured: C5 decode -5.5 % against a select
         // per symbol in the chain, 14 VALU instructions per step)
         const uint32_t sg = (uint32_t)__builtin_amdgcn_ds_bpermute((int)bj4, (int)sv);
         // symbols whose code lies inside the window (lane j + 1: the bits up to symbol j's end)
-        const uint32_t nval = __builtin_popcountll(ballot(sv <= n0) & (((1ull << kB) - 1) << 1));
+        const uint32_t nval = __builtin_popcountll(ballot(sv <= vlim) & (((1ull << kB) - 1) << 1));
         const uint32_t jmax = min(nval, (uint32_t)(i1 - i));
         // every symbol's whole root path at once, each group on its own window
         const uint32_t ent = opaque(*(const lds_u16 *)(size_t)(bvb + (((uint32_t)((w0 << sg) >> 32) >> bsh) << 1)));

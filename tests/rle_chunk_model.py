@@ -77,3 +77,132 @@ def pure_chunk(R, c):
         if i <= 255:
             out.append(255 if e == 257 else c)
     return bytes(out), (R + 256) % 258
+
+
+# ---- 1 KB blocks for run-heavy streams (hc_fgk.hip: rle_block) ----------------------------
+#
+# A full, non-final 1 KB block with few run starts (<= kSparseStarts) is coded by segments instead
+# of byte by byte. Its bytes split at the run starts p_0 < .. < p_{S-1}: the carried segment
+# [0, p_0) continues the run before the block (byte i at k = R + i, R the carried run counter) and
+# segment j = [p_j, p_{j+1}) is a new run (k = i - p_j). Per byte, with km = k mod 258:
+#   a run start emits [count R' - 3 if R' >= 3] + c   (R' = the run counter before it)
+#   otherwise km in {0, 1, 2} emits c, km == 257 emits 255, the rest nothing
+# so a segment emits, in order, its start's [count] + events at the offsets whose residue is in
+# {0, 1, 2, 257}: the t-th of those (after the count) is 255 when t % 4 == 3, else c (a new run:
+# residues 0, 1, 2, 257, 258 = 0, ...); the carried segment's start at residue R instead. The run
+# counter before start j is (R + p_0) mod 258 for j = 0 and L_{j-1} mod 258 after a new run of
+# length L_{j-1}. The kernel gives each start a lane and each event a lane (<= 63 events).
+kBlock = 1024
+kSparseStarts = 16
+
+
+def n_events(L):
+    """events of a new run's first L bytes (offsets with residue 0, 1, 2 or 257 mod 258)"""
+    return 4 * (L // 258) + min(L % 258, 3)
+
+
+def carried_events(R, L):
+    """the carried segment: symbols of its first L bytes (byte i at residue (R + i) mod 258), c
+    standing for the run byte (0x100) and 255 for a cut, in byte order (lane t of the kernel:
+    cycle t >> 2, entry t & 3 of the cyclic order 257, 0, 1, 2 rotated to start at R)"""
+    rot = R + 1 if R <= 2 else 0
+    out = []
+    for t in range(16):
+        q = (t + rot) & 3
+        e = 257 if q == 0 else q - 1
+        i = (e - R) % 258 + 258 * (t >> 2)
+        if i < L:
+            out.append(255 if e == 257 else 0x100)
+    return out
+
+
+def sparse_block(c, c_carry, R):
+    """c: the block's 1024 diffed bytes. Returns (symbols, R after the block), or None when the
+    block has more than kSparseStarts starts or more than 63 symbols (the kernel then codes it as
+    four 256-byte chunks)."""
+    c = np.asarray(c, dtype=np.int64)
+    prev = np.concatenate([[c_carry], c[:-1]])
+    start = c != prev
+    start[0] = start[0] or R == 0
+    p = np.flatnonzero(start)
+    S = p.size
+    if S > kSparseStarts:
+        return None
+    L0 = int(p[0]) if S else kBlock
+    syms = [c_carry if s == 0x100 else s for s in carried_events(R, L0)]
+    ends = list(p[1:]) + [kBlock]
+    for j in range(S):
+        L = int(ends[j] - p[j])
+        Rp = (R + int(p[0])) % 258 if j == 0 else int(p[j] - p[j - 1]) % 258
+        if Rp >= 3:
+            syms.append(Rp - 3)
+        syms += [255 if t % 4 == 3 else int(c[p[j]]) for t in range(n_events(L))]
+    if len(syms) > 63:
+        return None
+    Rn = (R + kBlock) % 258 if S == 0 else (kBlock - int(p[-1])) % 258
+    return bytes(syms), Rn
+
+
+def rle_blocked(data, diff=False):
+    """The kernel's chunk loop for a stream that fits one buffer window: 256-byte chunks
+    (rle_chunked's per-chunk rule) until a chunk has at most kSparseEnter starting lanes, then
+    1 KB blocks while they are sparse and four full chunks remain before the last one; a dense
+    block goes back to 256-byte chunks."""
+    data = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.int64)
+    n = data.size
+    nch = (n + 255) // 256
+    out = []
+    prev_x, R_carry, c_carry = 0, 0, 0
+    ci, sparse = 0, False
+
+    def diffed(x, px):
+        xp = np.concatenate([[px], x[:-1]])
+        return (x - xp) & 255 if diff else x.copy()
+
+    while ci < nch:
+        if sparse and ci + 4 < nch:
+            x = data[256 * ci:256 * ci + kBlock]
+            c = diffed(x, prev_x)
+            r = sparse_block(c, c_carry, R_carry)
+            if r is not None:
+                sym, R_carry = r
+                out += list(sym)
+                prev_x, c_carry = int(x[-1]), int(c[-1])
+                ci += 4
+                continue
+            sparse = False
+        base = 256 * ci
+        x = data[base:base + 256]
+        m = x.size
+        # one chunk of rle_chunked's loop, inline (same carry)
+        xp = np.concatenate([[prev_x], x[:-1]])
+        c = (x - xp) & 255 if diff else x.copy()
+        fin = base + m == n
+        cp = np.concatenate([[c_carry], c[:-1]])
+        same = c == cp
+        same[0] = R_carry > 0 and c[0] == c_carry
+        idx = np.arange(m)
+        starts = np.where(~same, idx, -1 << 30)
+        last_start = np.maximum.accumulate(np.maximum(starts, -R_carry))
+        k = idx - last_start
+        km = np.where(k >= 258, k - 258, k)
+        Rv = np.where(km == 257, 0, km + 1)
+        Rprev = np.concatenate([[R_carry], Rv[:-1]])
+        for i in range(m):
+            if (fin and i == m - 1) or km[i] == 0:
+                if Rprev[i] >= 3:
+                    out.append(int(Rprev[i] - 3))
+                out.append(int(c[i]))
+            elif km[i] in (1, 2):
+                out.append(int(c[i]))
+            elif km[i] == 257:
+                out.append(255)
+        # lanes (4 bytes each) holding a run start
+        lanes = len(set(int(i) >> 2 for i in np.flatnonzero(~same)))
+        sparse = lanes <= kSparseEnter
+        prev_x, R_carry, c_carry = int(x[-1]), int(Rv[-1]), int(c[-1])
+        ci += 1
+    return bytes(out)
+
+
+kSparseEnter = 2  # a 256-byte chunk whose run starts sit in at most this many lanes

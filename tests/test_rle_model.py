@@ -67,3 +67,39 @@ def test_pure_chunk_fast_path(oracle_mod):
                     raw = np.cumsum(np.frombuffer(raw, dtype=np.uint8), dtype=np.uint64).astype(np.uint8).tobytes()
                 want = oracle_mod.rle(oracle_mod.diff(raw) if diff else raw)
                 assert rle_chunked(raw, diff, fast=True) == want, (c, R, diff)
+
+
+def _run_heavy(rng, n):
+    """a stream of runs (lengths around the 258-byte cut and the 1 KB block) with sparse and dense
+    stretches, as raw bytes whose diff (or themselves) carry those runs"""
+    lens = [1, 2, 3, 4, 255, 256, 257, 258, 259, 260, 300, 515, 516, 517, 773, 1023, 1024, 1025, 2100]
+    parts, tot = [], 0
+    while tot < n:
+        if rng.random() < 0.15:  # a dense stretch
+            k = int(rng.integers(16, 700))
+            parts.append(rng.integers(0, 256, k).astype(np.uint8).tobytes())
+        else:
+            k = int(rng.choice(lens))
+            parts.append(bytes([int(rng.integers(0, 4))]) * k)
+        tot += k
+    return b"".join(parts)[:n]
+
+
+def test_blocked_rle_equals_serial(oracle_mod):
+    """the encoder's 1 KB sparse blocks (rle_chunk_model.rle_blocked, hc_fgk.hip rle_block) inside
+    the chunk loop equal the reference's FSM (transform.cpp:241-279): run-heavy streams with dense
+    stretches, every carried counter phase, both diff settings, and the grad photos"""
+    from rle_chunk_model import rle_blocked
+    rng = np.random.default_rng(5)
+    for t in range(160):
+        data = _run_heavy(rng, int(rng.integers(1, 24000)))
+        for diff in (False, True):
+            raw = data
+            if diff:  # a stream whose diff is `data`
+                raw = np.cumsum(np.frombuffer(data, dtype=np.uint8), dtype=np.uint64).astype(np.uint8).tobytes()
+            want = oracle_mod.rle(oracle_mod.diff(raw) if diff else raw)
+            assert rle_blocked(raw, diff) == want, (t, diff)
+    for k in range(3):
+        raw = oracle_mod.synth("grad", k, 512, 64).tobytes()
+        for diff in (False, True):
+            assert rle_blocked(raw, diff) == oracle_mod.rle(oracle_mod.diff(raw) if diff else raw)
