@@ -189,12 +189,6 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 #ifndef HC_DEC_EXIT8
 #define HC_DEC_EXIT8 1
 #endif
-#ifndef HC_DEC_DOUBLING
-#define HC_DEC_DOUBLING 1
-#endif
-#ifndef HC_DESCENT2
-#define HC_DESCENT2 1
-#endif
 #ifndef HC_BATCH_YIELD
 #define HC_BATCH_YIELD 5
 #endif
@@ -2104,7 +2098,6 @@ struct Dec {
             // the walk down on any inconsistency.
             // The window's bits are taken straight from a copy of it; the refill (and the 63-level
             // bound) is tested once per level against lim, the depth the bits in the window reach.
-#if HC_DESCENT2
             const uint32_t bbase = lds_off16(&fgk.T.body[0]);
             uint32_t xv = vreg(x), bv = vreg(b);
             if (in.nwin <= 32) in.refill();
@@ -2140,14 +2133,6 @@ struct Dec {
             in.nwin -= depth - d0;
             x = uni(xv);
             b = uni(bv);
-#else
-            do {
-                x = min((b & 255u) * 2 + in.bit(), x - 1);  // children sit below
-                pt = lane == 63 - depth ? x : pt;
-                ++depth;
-                b = uni(fgk.T.body[x]);
-            } while ((b & kInner) && depth < 63);
-#endif
             if (depth > 62) fgk.bad = 1;  // beyond the lanes (needs > 2^32 symbols)
             deep = depth > kInsertDepth;
             pv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((64 - depth + lane) & 63u) * 4), (int)pt);
@@ -2222,38 +2207,22 @@ struct Dec {
             return false;
         }
 #endif
-        // The chain by pointer doubling instead of seven serial steps (a lane read, a scalar add and
-        // a lane write each): lane o's next start nx = o + depth(o) (clamped to 63, exact below),
-        // nx2 = nx o nx and nx4 = nx2 o nx2 by two permutes, then lane j applies nx, nx2, nx4 by
-        // the bits of j (two more permutes): lane j <= 7 holds S_j. Values >= 63 were clamped, so a
-        // symbol counts as inside the window when its end is <= min(n0, 62).
-        static_assert(kB <= 7, "the doubling covers starts 0..7");
-        const uint32_t bj4 = bj * 4;
-#if HC_DEC_DOUBLING
-        const uint32_t nx = min(lane + dep, 63u);
-        const uint32_t nx2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nx * 4), (int)nx);
-        const uint32_t nx4 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nx2 * 4), (int)nx2);
-        uint32_t sv = sel(0xAAAAAAAAAAAAAAAAull, lane_read(nx, 0), 0u);  // lanes with bit 0: S_1
-        const uint32_t s2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sv * 4), (int)nx2);
-        sv = sel(0xCCCCCCCCCCCCCCCCull, s2, sv);
-        const uint32_t s4 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sv * 4), (int)nx4);
-        sv = sel(0xF0F0F0F0F0F0F0F0ull, s4, sv);
-        const uint32_t vlim = min(n0, 62u);
-#else
+        // (measured and dropped: the chain by pointer doubling -- lane o's next start o + depth(o),
+        // composed by permutes, lane j applying them by the bits of j: 11 VALU + 4 LDS instead of
+        // ~16 VALU + 7 SALU, but its dependent permutes made C5 decode +0.8 %)
         uint32_t S = 0, sv = 0;
+        const uint32_t bj4 = bj * 4;
 #pragma unroll
         for (uint32_t j = 0; j < kB; ++j) {
             sv = writelane(sv, S, j);
             S += lane_read(dep, S);
         }
         sv = writelane(sv, S, kB);
-        const uint32_t vlim = n0;
-#endif
         // each lane's own symbol's start: one permute (measured: C5 decode -5.5 % against a select
         // per symbol in the chain, 14 VALU instructions per step)
         const uint32_t sg = (uint32_t)__builtin_amdgcn_ds_bpermute((int)bj4, (int)sv);
         // symbols whose code lies inside the window (lane j + 1: the bits up to symbol j's end)
-        const uint32_t nval = __builtin_popcountll(ballot(sv <= vlim) & (((1ull << kB) - 1) << 1));
+        const uint32_t nval = __builtin_popcountll(ballot(sv <= n0) & (((1ull << kB) - 1) << 1));
         const uint32_t jmax = min(nval, (uint32_t)(i1 - i));
         // every symbol's whole root path at once, each group on its own window
         const uint32_t ent = opaque(*(const lds_u16 *)(size_t)(bvb + (((uint32_t)((w0 << sg) >> 32) >> bsh) << 1)));
