@@ -53,6 +53,24 @@ def test_batch_synthetic_512_digests(gpu, hc, oracle_mod, digests, mode):
     assert back == raws
 
 
+@pytest.mark.parametrize("mode", ["c", "cm"])
+def test_batch_synthetic_digests_full_launch(gpu, hc, oracle_mod, digests, mode):
+    """the same 12 reference outputs inside a batch of 264 streams: launches of more than
+    kLoneStreams (256) streams take the throughput kernels, smaller ones the latency variants
+    (hc_fgk.hip kLone), so both are pinned to the reference's digests"""
+    torch = gpu
+    names = sorted(digests["synthetic"])
+    base = [oracle_mod.synth(n.split("_")[0], int(n.split("_")[1])).tobytes() for n in names]
+    raws = base * 22
+    st, encs, _ = compress_batch(hc, torch, raws, use_diff=(mode == "cm"))
+    assert st == [0] * len(raws)
+    for k, e in enumerate(encs):
+        want = digests["synthetic"][names[k % len(names)]][mode]
+        assert (len(e), sha(e)) == (want["len"], want["sha256"]), k
+    st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
+    assert st == [0] * len(raws) and back == raws
+
+
 def test_batch_vs_oracle_mixed_sizes(gpu, hc, oracle_mod):
     """ragged batch: lengths not multiples of 4, tiny and empty streams, both modes"""
     torch = gpu
@@ -105,6 +123,22 @@ def test_batch_deep_and_skewed(gpu, hc, oracle_mod):
         for i, (r, e) in enumerate(zip(raws, encs)):
             ost, want = oracle_mod.compress(r, use_diff, False, 512)
             assert ost == 0 and e == want, (i, len(r), use_diff)
+        st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
+        assert st == [0] * len(raws) and back == raws
+
+
+def test_batch_deep_and_skewed_full_launch(gpu, hc, oracle_mod):
+    """the deep / skewed streams in a launch of more than kLoneStreams streams (the throughput
+    kernels; the test above, 11 streams, runs the latency variants)"""
+    torch = gpu
+    base = _deep_and_skewed()
+    raws = (base * (257 // len(base) + 1))[:260]
+    for use_diff in (False, True):
+        wants = [oracle_mod.compress(r, use_diff, False, 512) for r in base]
+        st, encs, _ = compress_batch(hc, torch, raws, use_diff)
+        assert st == [0] * len(raws)
+        for i, e in enumerate(encs):
+            assert wants[i % len(base)][0] == 0 and e == wants[i % len(base)][1], (i, use_diff)
         st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
         assert st == [0] * len(raws) and back == raws
 
