@@ -1281,11 +1281,7 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
     if (lane == 0) bt.status[sid] = cache ? kModeCache : kModeTables;
 }
 
-// kLone: the launch has few streams (launch_encode: at most kLoneStreams), so each wave's dependency
-// chain is its whole time; the batched hot path then reads the next batch's rows while the current
-// batch commits (speculating that the whole batch passes), at the price of reads wasted when it
-// does not (issue-bound full launches keep the plain loop)
-template <int kW, int kSrc, bool kTab = false, bool kLone = false>
+template <int kW, int kSrc, bool kTab = false>
 __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW, kTab>))) void encode_kernel(Batch bt)
 {
     __shared__ Tree<kW, false, kTab> trees[kWaves];
@@ -1482,17 +1478,13 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         const uint32_t svb = (uint32_t)(size_t)(const lds_u8 *)sb + bj;
         const uint32_t lkl = lane * kLv;
         uint32_t t = 0;
-        auto row_at = [&](uint32_t tt) __attribute__((always_inline)) {  // the rows of symbols tt..
-            const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + tt));
-            const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
-            return opaque(*(const lds_u16 *)(size_t)(rowb + 32 * (wh >> 10)));
-        };
-        uint32_t pos_next = 0;  // kLone: the rows of the batch at t, read during the last batch
-        bool have = false;
         while (t < ns) {
             if (sink.n > 64 - kBatch) sink.pack();
             const uint32_t jmax = min(kBatch, ns - t);
-            uint32_t pos = kLone && have ? pos_next : row_at(t);
+            const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + t));
+            const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
+            const uint32_t e = wh >> 10;
+            uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
             // lane 63 (idle) holds the root and adds one increment per batch symbol
             constexpr uint64_t kL63 = 1ull << 63;
             pos = sel(idle, kRoot, pos);
@@ -1504,9 +1496,6 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am, wa, scb), vinc, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
             const uint32_t wn = *(const lds_u32 *)(size_t)wa;
-            // where[] and the rows change only when a batch stops short (a miss, a walk): the
-            // next batch's rows, read now, are valid when this one passes whole
-            if constexpr (kLone) pos_next = row_at(t + jmax);
             // 2. the tests; 3. the increments from the first failing symbol on taken back
             const uint64_t fm = (ballot(w1 < wn) & am) | ballot(pos == kMissPos);
             const uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
@@ -1526,7 +1515,6 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             __builtin_amdgcn_wave_barrier();
             sink.n += jf;
             t += jf;
-            have = jf == jmax;
             if (jf < jmax) {  // symbol t: not cached, or a level reported: coded alone
                 if (sink.n == 64) sink.pack();
                 const uint32_t sym = uni(sb[t]);
@@ -1963,7 +1951,7 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
 // One stream's decoder (huffman.cpp:60-93 + transform.cpp:386-406 per symbol, then the RLE and
 // diff revert of transform.cpp:137-159 / 231-239 per 256-symbol block; header main.cpp:90-104).
 // decode_kernel runs one per wavefront.
-template <int kW, int kDst, bool kLone = false>
+template <int kW, int kDst>
 struct Dec {
     // symbol indices: 32-bit below 2^32 symbols (narrow / wide), 64-bit for the huge layout
     using Idx = std::conditional_t<kW == 2, uint64_t, uint32_t>;
@@ -1978,10 +1966,6 @@ struct Dec {
     uint8_t *sbuf;  // this block's symbols (LDS)
     Idx n;
     uint32_t bsym = 0, btry = 0;  // this block's batch symbols and batches
-    // kLone (launches of few streams): the next batch's level-8 reads, made during this batch on
-    // the window it leaves if it passes whole and needs no refill
-    bool spec = false;
-    uint32_t dep_next = 0;
     Prio<Idx> prio;
     bool batch_on = true;          // the next block runs batches
     uint64_t pacc = 0;  // HC_PROF regions
@@ -2214,11 +2198,7 @@ struct Dec {
         // lane o: the depth of a code that starts o bits into the window (its level-8 entry);
         // the chain of symbol starts then runs on registers: S_j+1 = S_j + depth(S_j). sv lane j:
         // the bits before symbol j.
-        auto dep_at = [&](uint64_t w) __attribute__((always_inline)) {
-            return opaque(*(const lds_u16 *)(size_t)(l8 + 2 * (uint32_t)((w << lane) >> 56))) >> 10;
-        };
-        const uint32_t dep = kLone && spec ? dep_next : dep_at(w0);
-        spec = false;
+        const uint32_t dep = opaque(*(const lds_u16 *)(size_t)(l8 + 2 * (uint32_t)((w0 << lane) >> 56))) >> 10;
 #if HC_DEC_EXIT8
         // a first code of 8 bits or more (most of them on a flat alphabet, e.g. noise, where codes
         // are longer than the tables) goes to the one-symbol step at once
@@ -2244,11 +2224,6 @@ struct Dec {
         // symbols whose code lies inside the window (lane j + 1: the bits up to symbol j's end)
         const uint32_t nval = __builtin_popcountll(ballot(sv <= n0) & (((1ull << kB) - 1) << 1));
         const uint32_t jmax = min(nval, (uint32_t)(i1 - i));
-        uint32_t smax = 0;
-        if constexpr (kLone) {  // the window after the whole batch, and its next level-8 reads
-            smax = lane_read(sv, jmax);
-            dep_next = dep_at(w0 << smax);
-        }
         // every symbol's whole root path at once, each group on its own window
         const uint32_t ent = opaque(*(const lds_u16 *)(size_t)(bvb + (((uint32_t)((w0 << sg) >> 32) >> bsh) << 1)));
         const uint32_t pos = ent & 1023u;
@@ -2281,7 +2256,6 @@ struct Dec {
         i += jf;
         bsym += jf;
         ++btry;
-        if constexpr (kLone) spec = jf == jmax && n0 - smax > 32;  // (the loop refills at <= 32)
         return jf == jmax;
     }
 #endif
@@ -2292,7 +2266,6 @@ struct Dec {
     template <bool kBat = (kW <= 1)>
     __device__ __forceinline__ void decode(Idx i0, Idx &i, Idx i1)
     {
-        spec = false;
         while (i < i1) {
             // huffman.cpp:60-93: the code's first 8 bits index the level tables: level 8 gives
             // where the walk from the root stops (depth d <= 8), the levels above give the
@@ -2301,7 +2274,6 @@ struct Dec {
                 HC_PROF_BEGIN();
                 fgk.build_levels();
                 HC_PROF_END(5);
-                spec = false;
             }
             if (in.nwin <= 32) in.refill();
 #if HC_DEC_BATCH
@@ -2438,7 +2410,7 @@ struct Dec {
     }
 };
 
-template <int kW, int kDst, bool kLone = false>
+template <int kW, int kDst>
 __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW>))) void decode_kernel(Batch bt)
 {
     __shared__ Tree<kW, true> trees[kWaves];
@@ -2447,7 +2419,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
     if (sid >= bt.n) return;
-    Dec<kW, kDst, kLone> dec(trees[wv], lane);
+    Dec<kW, kDst> dec(trees[wv], lane);
     if (!dec.open(bt, sid)) return;
     // two copies of the block loop, as in the encoder: without window bookkeeping for streams
     // that fit one window (input and output), with it for the rest
@@ -2469,9 +2441,6 @@ static uint32_t table_slots()
     return (uint32_t)cus * 24;
 }
 
-// launches of at most this many streams (one wave per CU or fewer) take the latency variants
-constexpr uint32_t kLoneStreams = 256;
-
 template <int kSrc>
 static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipStream_t st, hipStream_t aux)
 {
@@ -2488,8 +2457,7 @@ static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipSt
         aux = nullptr;
     hipStream_t ts = st;  // the table-mode launches' stream
     if (aux && hipEventRecord(fork, st) == hipSuccess && hipStreamWaitEvent(aux, fork, 0) == hipSuccess) ts = aux;
-    if (b.n <= kLoneStreams) encode_kernel<0, kSrc, false, true><<<grid, block, 0, st>>>(b);
-    else encode_kernel<0, kSrc><<<grid, block, 0, st>>>(b);
+    encode_kernel<0, kSrc><<<grid, block, 0, st>>>(b);
     encode_kernel<1, kSrc><<<grid, block, 0, st>>>(b);
     encode_kernel<2, kSrc><<<grid, block, 0, st>>>(b);
     encode_kernel<0, kSrc, true><<<grid, block, 0, ts>>>(b);
@@ -2532,13 +2500,11 @@ hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)
     b.min_tree = min_tree();
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
     if (dst == DST_RAW) {
-        if (b.n <= kLoneStreams) decode_kernel<0, DST_RAW, true><<<grid, block, 0, st>>>(b);
-        else decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_RAW><<<grid, block, 0, st>>>(b);
     } else {
-        if (b.n <= kLoneStreams) decode_kernel<0, DST_SYMBOLS, true><<<grid, block, 0, st>>>(b);
-        else decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
     }

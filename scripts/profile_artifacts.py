@@ -33,10 +33,14 @@ def kernel_key(name):
     """encode_kernel<0, 1, false> (tree layout 0 = narrow, source 1, path-cache mode; round-1 builds:
     <false, 1>) -> ('encode_kernel', narrow, source / destination kind). The table-mode launch of
     the same layout (<0, 1, true>) is keyed apart: on the -c -m headline its waves exit at once."""
-    m = re.search(r"(encode_kernel|decode_kernel)<(false|true|\d), (\d)(, (false|true))?>", name)
+    m = re.search(r"(encode_kernel|decode_kernel)<(false|true|\d), (\d)((?:, (?:false|true))*)>", name)
     if not m:
         return None
-    name = m.group(1) + ("_tables" if m.group(5) == "true" else "")
+    flags = [f.strip() == "true" for f in m.group(4).split(",")[1:]]
+    # encode_kernel<layout, source, kTab, kLone>, decode_kernel<layout, destination, kLone>
+    tab = m.group(1) == "encode_kernel" and len(flags) > 0 and flags[0]
+    lone = flags[-1] if (m.group(1) == "encode_kernel" and len(flags) > 1) or (m.group(1) == "decode_kernel" and flags) else False
+    name = m.group(1) + ("_tables" if tab else "") + ("_lone" if lone else "")
     return (name, m.group(2) in ("false", "0"), int(m.group(3)))
 
 

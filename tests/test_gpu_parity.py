@@ -55,9 +55,8 @@ def test_batch_synthetic_512_digests(gpu, hc, oracle_mod, digests, mode):
 
 @pytest.mark.parametrize("mode", ["c", "cm"])
 def test_batch_synthetic_digests_full_launch(gpu, hc, oracle_mod, digests, mode):
-    """the same 12 reference outputs inside a batch of 264 streams: launches of more than
-    kLoneStreams (256) streams take the throughput kernels, smaller ones the latency variants
-    (hc_fgk.hip kLone), so both are pinned to the reference's digests"""
+    """the same 12 reference outputs inside a batch of 264 streams (the same input in a launch
+    that fills more than one wave per CU, repeated streams in one launch)"""
     torch = gpu
     names = sorted(digests["synthetic"])
     base = [oracle_mod.synth(n.split("_")[0], int(n.split("_")[1])).tobytes() for n in names]
@@ -128,8 +127,7 @@ def test_batch_deep_and_skewed(gpu, hc, oracle_mod):
 
 
 def test_batch_deep_and_skewed_full_launch(gpu, hc, oracle_mod):
-    """the deep / skewed streams in a launch of more than kLoneStreams streams (the throughput
-    kernels; the test above, 11 streams, runs the latency variants)"""
+    """the deep / skewed streams repeated in a launch of 260 streams"""
     torch = gpu
     base = _deep_and_skewed()
     raws = (base * (257 // len(base) + 1))[:260]
