@@ -45,8 +45,10 @@ namespace {
 
 // Diagnostic build (-DHC_TC_PROF): tile_cost_kernel sums the s_memtime cycles of its phases
 // (load, equality words, candidates, summaries) into g_tc_prof (hc_debug_tc_prof reads it).
+// Slots 0-5: tile_cost (the tile_put barrier, its wait for the tile's loads, the rest of
+// tile_put, equality words, candidates, summaries); 8-11: emit_tile (the same three, the emit).
 #ifdef HC_TC_PROF
-__device__ unsigned long long g_tc_prof[4];
+__device__ unsigned long long g_tc_prof[16];
 #define HC_TC_BEGIN() uint64_t tc_t = __builtin_amdgcn_s_memtime()
 #define HC_TC_MARK(i)                                                                              \
     do {                                                                                           \
@@ -58,6 +60,10 @@ __device__ unsigned long long g_tc_prof[4];
 #define HC_TC_BEGIN()
 #define HC_TC_MARK(i)
 #endif
+// tile_put's phase marks (a no-op outside the HC_TC_PROF build)
+struct NoMark {
+    __device__ __forceinline__ void operator()(uint32_t) const {}
+};
 
 constexpr uint32_t kTile = 128;
 constexpr uint32_t kCand = 8;        // B = 8 << c, c = 0..7 (transform.cpp:294-328, <= 7 doublings)
@@ -632,8 +638,9 @@ __device__ __forceinline__ void tile_fetch(const TileAt &g, uint32_t *v, uint32_
         v[u] = whole ? *reinterpret_cast<const uint32_t *>(g.mat + lin) : (on ? load4(g.mat, lin, g.n) : 0u);
     }
 }
+template <class Mark = NoMark>
 __device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileAt &g, uint32_t *v, bool diff,
-                                         uint32_t tid)
+                                         uint32_t tid, Mark mark = {})
 {
     const uint32_t nd = (g.tw + 7) / 4, items = (g.th + 1) * nd;
     const uint32_t lane = tid & 63, wv = tid >> 6;
@@ -648,6 +655,11 @@ __device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileA
         }
     }
     lds_barrier();
+    mark(0);
+#ifdef HC_TC_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mark(1);
+#endif
     if (diff) {
 #pragma unroll
         for (uint32_t u = 0; u < kLU; ++u) {
@@ -670,6 +682,7 @@ __device__ __forceinline__ void tile_put(uint8_t *D, uint32_t *edge, const TileA
         }
     }
     lds_barrier();
+    mark(2);
 }
 
 // the value of lane l + d (d a power of two): DPP row_shl inside 16-lane rows, else a permute
@@ -883,7 +896,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
         const uint64_t pieces = M.pieces;
         HC_TC_BEGIN();
         // 1. the tile plus one row above and one column to the left, diff model applied
+#ifdef HC_TC_PROF
+        if (g.ok) tile_put(D, edge, g, v, diff, tid, [&](uint32_t k) { HC_TC_MARK(k + 1); });
+#else
         if (g.ok) tile_put(D, edge, g, v, diff, tid);
+#endif
         if (t + gridDim.x < ntiles) {
             nx = tile_at(a, ws, xcd_tile(t + gridDim.x, gridDim.x, ntiles));
             if (nx.ok) tile_fetch(nx, v, tid);
@@ -893,7 +910,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
         const uint64_t ntx = cdiv(W, kTile);
         const uint32_t tw = g.tw, th = g.th;
         const bool whole = tw == kTile && th == kTile;
-        HC_TC_MARK(1);
         // 2. Eh[r][k] bit j: x = tx0 + 64k + j equals x - 1 (row ty0 + r); Ev[c][k] bit j: y = ty0 +
         //    64k + j equals y - 1 (column tx0 + c). Eh: one word per thread from 16 dwords of its row
         //    (SWAR equality nibbles); Ev: lane = row, 4 ballots per dword column.
@@ -941,7 +957,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
         // (Eh / Ev by index into E, never as a selected pointer: a select of the two became a
         // scratch-memory pointer table and flat loads)
         constexpr uint32_t kEv = 2 * kTile;
-        HC_TC_MARK(2);
+        HC_TC_MARK(4);
         // 3. blocks of B <= 128, both scan orders
         //    (one copy per candidate: B, the lines per word and the group sizes are constants, so
         //    each thread's LDS reads unroll and issue together)
@@ -1108,7 +1124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
             const uint32_t w = readlane(wave_sum_incl(tot[c]), 63);
             if (lane == 0 && c < nct) atomicAdd(&M.total[c], (unsigned long long)w);
         }
-        HC_TC_MARK(3);
+        HC_TC_MARK(5);
         // 4. tile summaries for the blocks of B >= 256
         if (nc > kTileCand) {
             const uint64_t nty = cdiv(H, kTile);
@@ -1130,7 +1146,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
                     piece_pack(s, (uint32_t)(w[0] & 1), DT(1, x), DT(th, x));
             }
         }
-        HC_TC_MARK(4);  // (the next tile_put's first barrier ends this tile)
+        HC_TC_MARK(6);  // (the next tile_put's first barrier ends this tile)
     }
 }
 
@@ -1555,7 +1571,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE
         const uint32_t tid = tid_here(), lane = tid & 63, wv = tid >> 6;
         const TileAt g = nx;
         const bool want = wanted(g);
+        HC_TC_BEGIN();
+#ifdef HC_TC_PROF
+        if (want) tile_put(D, edge, g, v, diff, tid, [&](uint32_t k) { HC_TC_MARK(k + 9); });
+#else
         if (want) tile_put(D, edge, g, v, diff, tid);  // (its first barrier ends the previous tile)
+#endif
         if (t + gridDim.x < ntiles) {
             nx = tile_at(a, ws, xcd_tile(t + gridDim.x, gridDim.x, ntiles));
             if (wanted(nx)) tile_fetch(nx, v, tid);
@@ -1666,6 +1687,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE
                 }
             }
         }
+        HC_TC_MARK(12);
     }
 }
 
@@ -3845,9 +3867,9 @@ extern "C" int hc_debug_stage_times(char *names, int names_len, float *ms, int m
 #ifdef HC_TC_PROF
 extern "C" int hc_debug_tc_prof(unsigned long long *out, int reset)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_tc_prof), sizeof(unsigned long long) * 4) != hipSuccess) return 70;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_tc_prof), sizeof(unsigned long long) * 16) != hipSuccess) return 70;
     if (reset) {
-        unsigned long long z[4] = {0, 0, 0, 0};
+        unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_tc_prof), z, sizeof(z)) != hipSuccess) return 70;
     }
     return 0;

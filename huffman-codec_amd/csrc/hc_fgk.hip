@@ -1219,8 +1219,11 @@ struct RecSink {
 // Waves per SIMD each tree layout's LDS admits (8 four-wave workgroups per CU narrow, 6 wide, 4
 // huge): the register budget the compiler may use (fewer scalar spills in the wide kernels,
 // which C4's single long stream runs)
+#ifndef HC_WPE0
+#define HC_WPE0 8
+#endif
 template <int kW, bool kTab = false>
-constexpr int kWavesPerSimd = kTab ? (kW == 0 ? 6 : 5) : (kW == 0 ? 8 : (kW == 1 ? 6 : 4));
+constexpr int kWavesPerSimd = kTab ? (kW == 0 ? 6 : 5) : (kW == 0 ? HC_WPE0 : (kW == 1 ? 6 : 4));
 
 // Which way the encoder finds codes, voted per stream (status[] carries the vote until the
 // encoder overwrites it with the stream's status; the two modes' launches run side by side on two
@@ -1247,20 +1250,31 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
     uint32_t *h = hist[wv];
     for (uint32_t i = lane; i < 256; i += 64) h[i] = 0;
     __builtin_amdgcn_wave_barrier();
-    const uint8_t *in = bt.in + bt.in_offs[sid];
     const uint64_t n = bt.in_lens[sid];
     const uint32_t m = (uint32_t)min(n, (uint64_t)16384);
-    uint32_t prev = 0, total = 0;  // the byte before this lane's, run starts
-    for (uint32_t b = 0; b < m; b += 64) {
-        const uint32_t i = b + lane;
-        uint32_t v = i < m ? in[i] : 0u;
-        if (kSrc == SRC_RAW_DIFF) v = (v - (i ? (i - 1 < m ? in[i - 1] : 0u) : 0u)) & 255u;
-        const uint32_t up = __shfl_up(v, 1, 64);
-        const uint32_t pv = lane == 0 ? prev : up;
-        const bool start = i < m && (i == 0 || v != pv);
-        if (start) atomicAdd(&h[v], 1u);
-        total += (uint32_t)__builtin_popcountll(ballot(start));
-        prev = lane_read(v, 63);
+    // four bytes per lane and step, one dword load (the bytes of its last dword past m are
+    // masked off); the previous byte of each comes from the dword before (lane - 1, or lane 63
+    // of the step before)
+    const rsrc_t rs = make_rsrc(bt.in + bt.in_offs[sid], (m + 3u) & ~3u);
+    uint32_t prev_raw = 0, prev_sym = 0, total = 0;  // lane 63's dwords of the last step; run starts
+    for (uint32_t b = 0; b < m; b += 256) {
+        const uint32_t i = b + 4 * lane;
+        const uint32_t w = buf_load(rs, i);
+        uint32_t sy = w;
+        if (kSrc == SRC_RAW_DIFF) {  // transform.cpp:220-229 (m[-1] = 0), bytewise
+            const uint32_t xp = (w << 8) | (wave_shr1(w, prev_raw) >> 24);
+            sy = ((w | 0x80808080u) - (xp & 0x7F7F7F7Fu)) ^ ((w ^ ~xp) & 0x80808080u);
+            prev_raw = lane_read(w, 63);
+        }
+        const uint32_t sp = (sy << 8) | (wave_shr1(sy, prev_sym) >> 24);
+        prev_sym = lane_read(sy, 63);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t v = byte_of(sy, k);
+            const bool start = i + k < m && (i + k == 0 || v != byte_of(sp, k));
+            if (start) atomicAdd(&h[v], 1u);
+            total += (uint32_t)__builtin_popcountll(ballot(start));
+        }
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t c[4], top = 0;

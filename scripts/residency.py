@@ -89,6 +89,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--streams", type=int, default=8192)
     ap.add_argument("--kind", default="photo")
+    ap.add_argument("--no-diff", action="store_true")
     args = ap.parse_args()
     import torch
     import hcodec as hc
@@ -111,11 +112,11 @@ def main():
     bst = torch.zeros_like(est)
     trace = torch.zeros(3 * S, dtype=torch.int64, device=dev)
     # warm run without the trace
-    hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, est, use_diff=True)
+    hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, est, use_diff=not args.no_diff)
     torch.cuda.synchronize()
     assert L.hc_debug_set_trace(ctypes.c_void_p(trace.data_ptr())) == 0
     try:
-        hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, est, use_diff=True)
+        hc.compress_batch(raw, offs, lens, enc, eoffs, ecaps, elens, est, use_diff=not args.no_diff)
         torch.cuda.synchronize()
         analyze("encode_kernel", trace.view(S, 3).cpu().numpy())
         trace.zero_()

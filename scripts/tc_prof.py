@@ -1,6 +1,7 @@
-"""Phase shares of tile_cost_kernel (diagnostic; needs a -DHC_TC_PROF build via HC_LIB_PATH).
+"""Phase shares of tile_cost_kernel and emit_tile_kernel (diagnostic; needs a -DHC_TC_PROF build,
+scripts/build_var.sh TCP -DHC_TC_PROF, loaded through HC_LIB_PATH).
 
-    HC_LIB_PATH=abvar/TCP/libhcodec.so python scripts/tc_prof.py [--streams 8192]
+    HC_LIB_PATH=abvar/TCP/libhcodec_dbg.so python scripts/tc_prof.py [--streams 8192]
 """
 import argparse
 import ctypes
@@ -36,17 +37,20 @@ def main():
     elens = torch.zeros(S, **i64)
     est = torch.zeros(S, dtype=torch.int32, device=dev)
     work = None
-    buf = (ctypes.c_ulonglong * 4)()
+    buf = (ctypes.c_ulonglong * 16)()
     for it in range(3):
         work = hc.compress_adapt_batch(raw, offs, lens, widths, enc, eoffs, ecaps, elens, est,
                                        use_diff=not a.no_diff, work=work)
         torch.cuda.synchronize()
         L.hc_debug_tc_prof(ctypes.cast(buf, ctypes.c_void_p), 1)
-    tot = sum(buf)
-    names = ["load tile", "equality words", "candidates B<=128", "summaries + sync"]
-    print({n: round(100 * v / tot, 1) for n, v in zip(names, buf)}, "cycles per tile (WG thread 0):",
-          round(tot / (S * (a.side // 128) ** 2)))
-
+    tiles = S * (a.side // 128) ** 2
+    for name, lo, phases in (("tile_cost", 0, ["put barrier", "put load wait", "put diff+store", "equality words",
+                                               "candidates B<=128", "summaries"]),
+                             ("emit_tile", 8, ["put barrier", "put load wait", "put diff+store", "emit"])):
+        vals = list(buf[lo:lo + len(phases)])
+        tot = sum(vals) or 1
+        print(name, {n: round(100 * v / tot, 1) for n, v in zip(phases, vals)},
+              "cycles per tile (WG thread 0):", round(tot / tiles))
 
 if __name__ == "__main__":
     main()
