@@ -1228,13 +1228,14 @@ constexpr int kWavesPerSimd = kTab ? (kW == 0 ? 6 : 5) : (kW == 0 ? HC_WPE0 : (k
 // Which way the encoder finds codes, voted per stream (status[] carries the vote until the
 // encoder overwrites it with the stream's status; the two modes' launches run side by side on two
 // HIP streams, launch_encode_src): the path cache when the stream's 16 most frequent
-// symbols cover most of it (>= 60 %: the diff model's photos, 96 %), the level tables when the
-// alphabet is flat (< 15 %: noise, ramps, 6-8 %) -- measured: photo -c -m 8192 streams cache 67
+// symbols cover most of it (>= 60 %: the diff model's photos, 95 %), the level tables when the
+// alphabet is flat (< 9 %: noise, ramps, 6-8 %) -- measured: photo -c -m 8192 streams cache 67
 // ms / tables 131, noise -c -m 2048 485 / 227, ramps -c 8192 623 / 365 -- and in between (photos
-// without the diff model, ~25 %) the tables only when every stream is resident at once in table
-// mode's occupancy (photo -c 4096 streams 325 / 231 ms, 8192 401 / 436; the 4096^2 -c -a
-// matrix, one stream, 6.25 / 2.97 s). Estimated from the first 16 KB: the byte of every run
-// start (diff model applied), a 256-bin histogram per wave in LDS, the top 16 by repeated max.
+// without the diff model, 10-13 %; hd01 -c -m 41 %) the tables only when every stream is
+// resident at once in table mode's occupancy (photo -c 4096 streams 325 / 231 ms, 8192 401 /
+// 436; the 4096^2 -c -a matrix, one stream, 6.25 / 2.97 s; hd01 -c -m alone 108 / 55 ms).
+// Estimated from a sample of 16 KB (below): the byte of every run start (diff model applied), a
+// 256-bin histogram per wave in LDS, the top 16 by repeated max.
 constexpr int32_t kModeTables = -0x7A0, kModeCache = -0x7A1;
 template <int kSrc>
 __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_occ, uint32_t forced)
@@ -1251,15 +1252,22 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
     for (uint32_t i = lane; i < 256; i += 64) h[i] = 0;
     __builtin_amdgcn_wave_barrier();
     const uint64_t n = bt.in_lens[sid];
-    const uint32_t m = (uint32_t)min(n, (uint64_t)16384);
-    // four bytes per lane and step, one dword load (the bytes of its last dword past m are
-    // masked off); the previous byte of each comes from the dword before (lane - 1, or lane 63
-    // of the step before)
-    const rsrc_t rs = make_rsrc(bt.in + bt.in_offs[sid], (m + 3u) & ~3u);
-    uint32_t prev_raw = 0, prev_sym = 0, total = 0;  // lane 63's dwords of the last step; run starts
-    for (uint32_t b = 0; b < m; b += 256) {
-        const uint32_t i = b + 4 * lane;
-        const uint32_t w = buf_load(rs, i);
+    const uint8_t *const in = bt.in + bt.in_offs[sid];
+    // The sample: a stream of <= 16 KB whole, a longer one as 64 segments of 256 bytes spread
+    // evenly over it (its first 16 KB alone misjudged hd01 -c -m, a flat top and then a wide
+    // alphabet: cache 108 ms against tables 55 ms as a lone stream). Four bytes per lane and
+    // segment, one dword load (the bytes of a last dword past the stream masked off); each byte's
+    // previous byte comes from the dword before (lane - 1, lane 63 of the segment before when they
+    // are contiguous, else the byte before the segment) and a spread segment's first symbol
+    // starts a run.
+    const bool spread = n > 16384;
+    const uint32_t nseg = spread ? 64u : (uint32_t)((n + 255) / 256);
+    uint32_t prev_raw = 0, prev_sym = 0, total = 0;  // lane 63's dwords of the last segment; run starts
+    for (uint32_t k = 0; k < nseg; ++k) {
+        const uint64_t o = spread ? ((n - 256) * k / 63) & ~3ull : 256ull * k;
+        const uint32_t len = (uint32_t)min(n - o, (uint64_t)256);
+        const uint32_t w = buf_load(make_rsrc(in + o, (len + 3u) & ~3u), 4 * lane);
+        if (spread) prev_raw = o ? (uint32_t)in[o - 1] << 24 : 0u;
         uint32_t sy = w;
         if (kSrc == SRC_RAW_DIFF) {  // transform.cpp:220-229 (m[-1] = 0), bytewise
             const uint32_t xp = (w << 8) | (wave_shr1(w, prev_raw) >> 24);
@@ -1268,10 +1276,11 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
         }
         const uint32_t sp = (sy << 8) | (wave_shr1(sy, prev_sym) >> 24);
         prev_sym = lane_read(sy, 63);
+        const bool first = spread || k == 0;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t v = byte_of(sy, k);
-            const bool start = i + k < m && (i + k == 0 || v != byte_of(sp, k));
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t i = 4 * lane + j, v = byte_of(sy, j);
+            const bool start = i < len && ((first && i == 0) || v != byte_of(sp, j));
             if (start) atomicAdd(&h[v], 1u);
             total += (uint32_t)__builtin_popcountll(ballot(start));
         }
@@ -1291,7 +1300,7 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
             else c[3] = 0;
         }
     }
-    const bool cache = total == 0 || 100ull * top >= 60ull * total || (100ull * top >= 15ull * total && !low_occ);
+    const bool cache = total == 0 || 100ull * top >= 60ull * total || (100ull * top >= 9ull * total && !low_occ);
     if (lane == 0) bt.status[sid] = cache ? kModeCache : kModeTables;
 }
 
@@ -2548,6 +2557,24 @@ extern "C" int hc_debug_set_enc_tab(uint32_t mode)
     // 0: per stream (sampled alphabet), 1: path cache for every stream, 2: tables for every stream
     hc::g_enc_tab = mode > 2 ? 0 : mode;
     return 0;
+}
+
+extern "C" int hc_debug_enc_votes(const uint8_t *in, const uint64_t *in_offs, const uint64_t *in_lens, uint32_t n,
+                                  uint32_t flags, uint32_t low_occ, int32_t *status, void *stream)
+{
+    // enc_mode_kernel alone: status[i] = the vote (kModeCache -0x7A1 / kModeTables -0x7A0)
+    hc::Batch b{};
+    b.in = in;
+    b.in_offs = in_offs;
+    b.in_lens = in_lens;
+    b.n = n;
+    b.status = status;
+    b.flags = flags;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) return 0;
+    if (flags & HC_FLAG_DIFF) hc::enc_mode_kernel<hc::SRC_RAW_DIFF><<<(n + 3) / 4, 256, 0, st>>>(b, low_occ, 0u);
+    else hc::enc_mode_kernel<hc::SRC_RAW><<<(n + 3) / 4, 256, 0, st>>>(b, low_occ, 0u);
+    return hipGetLastError() == hipSuccess ? 0 : HC_ERR_DEVICE;
 }
 
 extern "C" int hc_debug_set_trace(void *dev_buf)

@@ -388,6 +388,19 @@ def debug_set_enc_tab(mode):
         raise HCodecError(f"hc_debug_set_enc_tab failed: {rc}")
 
 
+def debug_enc_votes(inp, in_offs, in_lens, use_diff, low_occ, status, stream=None):
+    """Test hook (debug build only, use_debug_build): the encoder's per-stream mode vote alone
+    (enc_mode_kernel) into status: -0x7A1 the path cache, -0x7A0 the level tables. low_occ: the
+    batch fits table mode's residency (what the launcher passes for <= 24 streams per CU)."""
+    n = _check_batch(inp, in_offs, in_lens, inp, in_offs, in_lens, in_lens, status)
+    f = _dbg().hc_debug_enc_votes
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 3 + [ctypes.c_void_p] * 2
+    rc = f(_dp(inp), _dp(in_offs), _dp(in_lens), n, HC_FLAG_DIFF if use_diff else 0, 1 if low_occ else 0, _dp(status),
+           _stream_handle(stream))
+    if rc:
+        raise HCodecError(f"hc_debug_enc_votes failed: {rc}")
+
+
 def debug_set_par_min(symbols):
     """Test hook (debug build only, use_debug_build): adaptive streams of at least `symbols` block
     symbols find their block boundaries by the parallel pass (default 2^20; 0: every stream)."""
