@@ -2,9 +2,12 @@
 """bench.py — encode+decode GiB/s of the MI355X huffman-codec on batched 512x512 .raw streams.
 
 Headline workload = BASELINE.json configs[4] (C5): a batch of 65536 synthetic 512x512 photo
-streams (seed 0x5EED, generated in HBM), sharded across the ranks
-(strong scaling: rank r owns streams [r*S, (r+1)*S), S = 65536 / N; at N=1 the GPU codes the
-whole C5 batch). One step is the reference's full round trip on the shard: `-c -m` encode
+streams (seed 0x5EED, generated in HBM) per GPU. The streams are
+independent units, so N GPUs code N such batches, one per rank, with no data-path collective
+(weak scaling, per-GPU work fixed: rank r owns streams [r*S, (r+1)*S) of the global sequence, S =
+65536; at N=1 the GPU codes exactly the C5 batch). --total-streams T instead splits one batch of T
+streams over the ranks (strong scaling; T = 65536 is C5's batch spread over N GPUs: at N=8 each
+GPU then holds 8192 streams, a single round of wavefronts that ends with its slowest stream). One step is the reference's full round trip on the shard: `-c -m` encode
 (diff -> MNP-5 RLE -> FGK -> header, one fused kernel) then decode (FGK -> RLE revert -> diff
 revert, one fused kernel). value = raw bytes of all ranks / step time (max over ranks), GiB/s.
 After the timed region: every status 0, decode == input on every stream, and (rank 0, N=1) the
@@ -50,7 +53,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--streams", type=int, default=C5_STREAMS, help="streams in the whole batch (all ranks)")
+    ap.add_argument("--streams", type=int, default=C5_STREAMS, help="streams per GPU (weak scaling)")
+    ap.add_argument("--total-streams", type=int, default=0,
+                    help="strong scaling instead: streams in the whole batch, split over the ranks")
     ap.add_argument("--kind", default="photo", choices=["photo", "grad", "noise"])
     ap.add_argument("--no-diff", action="store_true", help="-c instead of -c -m")
     ap.add_argument("--cpu-sample", type=int, default=0, help="streams for the CPU baseline (0 = auto)")
@@ -718,9 +723,11 @@ def main(argv=None):
         print(json.dumps({"configs": res, "bad": bad}), flush=True)
         raise SystemExit(1 if bad else 0)
 
-    if args.streams % world:
-        raise SystemExit(f"--streams {args.streams} does not split over {world} ranks")
-    S = args.streams // world
+    strong = args.total_streams > 0
+    if strong and args.total_streams % world:
+        raise SystemExit(f"--total-streams {args.total_streams} does not split over {world} ranks")
+    S = args.total_streams // world if strong else args.streams
+    total = world * S
     use_diff = not args.no_diff
     N = args.dry_stream_bytes if dry else N_RAW
     b = StandInBatch(torch, rank * S, S, N) if dry else Batch(torch, hc, dev, args.kind, rank * S, S, use_diff)
@@ -743,11 +750,11 @@ def main(argv=None):
     result = {
         "metric": METRIC, "value": round(value, 4), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8",
         "data": f"synthetic {args.kind} (SURVEY.md App. D, seed 0x5EED), generated in HBM",
-        "config": {"workload": f"C5: {args.streams} x 512x512 {args.kind} streams over {world} GPU(s) "
+        "config": {"workload": f"C5: {total} x 512x512 {args.kind} streams over {world} GPU(s) "
                                f"({S} per GPU), {'-c -m' if use_diff else '-c'} encode + decode round trip",
-                   "streams_total": args.streams, "streams_per_gpu": S, "stream_bytes": N,
+                   "streams_total": total, "streams_per_gpu": S, "stream_bytes": N,
                    "mode": "-c -m" if use_diff else "-c",
                    "parallelism": f"dp{world} (stream shards, no data-path collective)"},
         "roofline": roof, "issue": issue,
@@ -761,7 +768,7 @@ def main(argv=None):
         result.update({"metric": METRIC + " [gloo dry run: streams copied, not coded]", "dry_run": True,
                        "backend": "gloo", "bit_exact": None, "fgk_symbols_per_stream": None,
                        "data": "stand-in: pseudo-random bytes per stream (torch generator seeded by the stream index)"})
-        result["config"]["workload"] = f"dry run: {args.streams} x {N}-byte streams over {world} rank(s) ({S} per rank)"
+        result["config"]["workload"] = f"dry run: {total} x {N}-byte streams over {world} rank(s) ({S} per rank)"
     if dist.is_initialized():
         result["process_group"] = {"backend": dist.get_backend(), "world": dist.get_world_size()}
     if world == 1 and not dry:

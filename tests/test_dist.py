@@ -97,12 +97,13 @@ def test_pack_single_process():
     assert hcdist.pack(buf, offs, lens).tolist() == [0, 1, 2, 30, 31, 32, 33, 34]
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_bench_multi_rank_dry_run(world):
+@pytest.mark.parametrize("world,strong", [(1, False), (2, False), (3, False), (2, True)])
+def test_bench_multi_rank_dry_run(world, strong):
     """bench.py's own multi-rank path (shards, barriers, max-over-ranks timing, counter reduction,
     --gather) end to end under the driver's launcher, on CPU: --backend gloo swaps each rank's GPU
     step for a stand-in that copies its streams. Rank 0 prints exactly one JSON line; the gathered
-    payload is every rank's shard in global stream order."""
+    payload is every rank's shard in global stream order. Weak scaling (the headline: --streams per
+    GPU) and strong scaling (--total-streams split over the ranks) shard the same way."""
     import hashlib
     import json
     import subprocess
@@ -112,8 +113,8 @@ def test_bench_multi_rank_dry_run(world):
     S, N = 2 * world, 3000
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--backend", "gloo", "--gpus", str(world), "--streams", str(S), "--steps", "3", "--warmup", "1",
-           "--gather", "--dry-stream-bytes", str(N)]
+           "--backend", "gloo", "--gpus", str(world), "--steps", "3", "--warmup", "1",
+           "--gather", "--dry-stream-bytes", str(N)] + (["--total-streams", str(S)] if strong else ["--streams", "2"])
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -124,7 +125,7 @@ def test_bench_multi_rank_dry_run(world):
     # the launcher's process group exists at world 1 too (the RCCL path on a one-GPU box)
     assert r["process_group"] == {"backend": "gloo", "world": world}
     assert r["config"]["streams_total"] == S and r["config"]["streams_per_gpu"] == 2
-    assert r["value"] > 0 and r["ms_per_step"] > 0 and r["scaling"] == "strong"
+    assert r["value"] > 0 and r["ms_per_step"] > 0 and r["scaling"] == ("strong" if strong else "weak")
     assert r["bits_per_byte"] == 8.0  # the stand-in copies: encoded = raw bytes
     sys.path.insert(0, root)
     import bench
