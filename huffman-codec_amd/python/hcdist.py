@@ -14,8 +14,8 @@ import torch.distributed as dist
 
 def shard(rank, world, per_rank):
     """Global stream indices owned by `rank`: the contiguous range [rank * per_rank, (rank + 1) * per_rank).
-    bench.py splits a fixed total over the ranks (strong scaling: per_rank = total / world); a
-    caller that fixes per_rank instead scales weakly."""
+    bench.py fixes per_rank (one C5 batch per GPU: weak scaling) by default, and with
+    --total-streams splits a fixed total over the ranks (strong scaling: per_rank = total / world)."""
     return range(rank * per_rank, (rank + 1) * per_rank)
 
 
