@@ -876,7 +876,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_TC_WPE))
     __shared__ uint32_t st128[2][4][3];       // stats128
     __shared__ uint32_t HV[682];              // whole tiles: every candidate's block costs (h then v)
     __shared__ uint32_t edge[4 * kLU];        // tile_put
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t tid = threadIdx.x;  // (lane and wave: per tile, tid_here)
     const uint64_t ntiles = ws.ctr[0];
     const bool diff = a.diff != 0;
     // the next tile's raw dwords are in flight while this one is worked on
@@ -1555,7 +1555,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC_EMIT_WPE
 {
     __shared__ uint8_t D[(kTile + 1) * kDS];
     __shared__ uint32_t edge[4 * kLU];  // tile_put
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t tid = threadIdx.x;  // (lane and wave: per tile, tid_here)
     const uint64_t ntiles = ws.ctr[0];
     const bool diff = a.diff != 0;
     // the next tile's raw dwords are in flight while this one is emitted (tile_fetch / tile_put,
