@@ -1014,41 +1014,51 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
     return at + total;
 }
 
-// A full, non-final 1 KB block of a run-heavy stream (tests/rle_chunk_model.py: sparse_block,
-// rle_blocked), lane l holding bytes 16 l .. 16 l + 15 in x[0..3] (one 16-byte load). When the
-// block has at most kSparseStarts run starts and at most 63 symbols, it is coded by segments
-// instead of byte by byte: the carried segment [0, p_0) continues the run before the block, and
-// segment j = [p_j, p_j+1) is a new run. A segment emits its start's count (when the run before
-// it reached R' >= 3: R' - 3) and c, then a symbol for every offset whose residue mod 258 is 0, 1,
-// 2 (c) or 257 (255): the t-th of those is 255 when t % 4 == 3. The carried segment's residues
-// start at the carried counter R instead. Lane j < S holds start j (its segment's length and
-// event count), a scan of the counts places the segments, and each symbol's lane finds its
+// A full, non-final block of kQ KB of a run-heavy stream (tests/rle_chunk_model.py: sparse_block,
+// rle_blocked), lane l holding bytes 16 kQ l .. 16 kQ l + 16 kQ - 1 in x[0..4 kQ) (kQ 16-byte
+// loads). When the block has at most kSparseStarts run starts and at most 63 symbols, it is coded
+// by segments instead of byte by byte: the carried segment [0, p_0) continues the run before the
+// block, and segment j = [p_j, p_j+1) is a new run. A segment emits its start's count (when the
+// run before it reached R' >= 3: R' - 3) and c, then a symbol for every offset whose residue mod
+// 258 is 0, 1, 2 (c) or 257 (255): the t-th of those is 255 when t % 4 == 3. The carried segment's
+// residues start at the carried counter R instead. Lane j < S holds start j (its segment's length
+// and event count), a scan of the counts places the segments, and each symbol's lane finds its
 // segment by a max-scan over markers (one LDS row). Returns the symbols pending after the block,
-// or kDense with nothing written and the carry unchanged (the caller then codes the block as four
+// or kDense with nothing written and the carry unchanged (the caller then codes the block as
 // 256-byte chunks). The caller guarantees room for 63 symbols.
 #ifndef HC_SPARSE
 #define HC_SPARSE 1
 #endif
+// KB per sparse block (1 or 2): 2 halves the blocks of a run-heavy stream (grad: every 2 KB block
+// stays within the 16 starts and 63 symbols, slot-form model), 4 KB would not fit them
+#ifndef HC_SPARSE_KB
+#define HC_SPARSE_KB 2
+#endif
 constexpr uint32_t kSparseStarts = 16;
 constexpr uint32_t kDense = 0xFFFFFFFFu;
-template <int kSrc>
-__device__ __forceinline__ uint32_t rle_block(const u32x4 x, RleCarry &cy, uint8_t *sb, uint32_t at, uint32_t *row,
+template <int kSrc, uint32_t kQ>
+__device__ __forceinline__ uint32_t rle_block(const u32x4 *blk, RleCarry &cy, uint8_t *sb, uint32_t at, uint32_t *row,
                                               uint32_t lane)
 {
-    // transform.cpp:220-229: the diffed bytes (lane 0's previous byte is the carry's)
-    uint32_t c[4];
-    uint32_t pb = wave_shr1(x[3], cy.x << 24) >> 24;
+    constexpr uint32_t kX = 4 * kQ;          // dwords per lane
+    constexpr uint32_t kBytes = 1024 * kQ;   // bytes per block
+    uint32_t x[kX];
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
+    for (uint32_t k = 0; k < kX; ++k) x[k] = blk[k >> 2][k & 3];
+    // transform.cpp:220-229: the diffed bytes (lane 0's previous byte is the carry's)
+    uint32_t c[kX];
+    uint32_t pb = wave_shr1(x[kX - 1], cy.x << 24) >> 24;
+#pragma unroll
+    for (uint32_t k = 0; k < kX; ++k) {
         const uint32_t xp = (x[k] << 8) | pb;
         c[k] = kSrc == SRC_RAW_DIFF ? (((x[k] | 0x80808080u) - (xp & 0x7F7F7F7Fu)) ^ ((x[k] ^ ~xp) & 0x80808080u)) : x[k];
         pb = x[k] >> 24;
     }
     // run starts: bit 4 k + b of M for byte b of c[k] (byte 0 of the block also when R = 0: a cut)
     uint32_t M = 0;
-    pb = wave_shr1(c[3], cy.c << 24) >> 24;
+    pb = wave_shr1(c[kX - 1], cy.c << 24) >> 24;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
+    for (uint32_t k = 0; k < kX; ++k) {
         const uint32_t d = c[k] ^ ((c[k] << 8) | pb);
         const uint32_t f = ((((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u) >> 7;  // 1 per nonzero byte
         M |= ((f | (f >> 7) | (f >> 14) | (f >> 21)) & 15u) << (4 * k);
@@ -1063,9 +1073,11 @@ __device__ __forceinline__ uint32_t rle_block(const u32x4 x, RleCarry &cy, uint8
     {
         uint32_t r = incl - cnt, m = M;
         while (ballot(m != 0)) {
-            const uint32_t b = (uint32_t)__builtin_ctz(m | 0x10000u);
-            const uint32_t ck = (b & 8u) ? ((b & 4u) ? c[3] : c[2]) : ((b & 4u) ? c[1] : c[0]);
-            row[m ? r : 63u] = (lane * 16 + b) | (((ck >> (8 * (b & 3u))) & 255u) << 16);
+            const uint32_t b = m ? (uint32_t)__builtin_ctz(m) : 0u;
+            uint32_t ck = c[0];
+#pragma unroll
+            for (uint32_t k = 1; k < kX; ++k) ck = (b >> 2) == k ? c[k] : ck;
+            row[m ? r : 63u] = (lane * 4 * kX + b) | (((ck >> (8 * (b & 3u))) & 255u) << 16);
             r += m ? 1u : 0u;
             m &= m - 1u;
         }
@@ -1073,16 +1085,16 @@ __device__ __forceinline__ uint32_t rle_block(const u32x4 x, RleCarry &cy, uint8
     __builtin_amdgcn_wave_barrier();
     const uint32_t pw = row[lane];
     const bool st = lane < S;
-    const uint32_t p = st ? pw & 0xFFFFu : 1024u;
+    const uint32_t p = st ? pw & 0xFFFFu : kBytes;
     const uint32_t cb = (pw >> 16) & 255u;
     const uint32_t R0 = cy.R;
-    const uint32_t p0 = S ? lane_read(p, 0) : 1024u;
+    const uint32_t p0 = S ? lane_read(p, 0) : kBytes;
     // segment j: [p, pn); the run counter before its start: (R0 + p_0) mod 258 for j = 0, the
     // previous new run's length mod 258 otherwise
-    const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(1024, (int)p, 0x130, 0xF, 0xF, false);  // wave_shl:1
+    const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp((int)kBytes, (int)p, 0x130, 0xF, 0xF, false);  // wave_shl:1
     const uint32_t pp = wave_shr1(p, 0u);
     const uint32_t L = pn - p;
-    auto mod258 = [](uint32_t v) {  // v < 1290
+    auto mod258 = [](uint32_t v) {  // v < 2321 (the largest here: R0 + 2048 < 2306)
         return v - 258u * ((v * 2033u) >> 19);
     };
     const uint32_t Rp = mod258(lane == 0 ? R0 + p : p - pp);
@@ -1090,13 +1102,13 @@ __device__ __forceinline__ uint32_t rle_block(const u32x4 x, RleCarry &cy, uint8
     const uint32_t qL = (L * 2033u) >> 19;
     const uint32_t ne = st ? hc + 4 * qL + min(L - 258u * qL, 3u) : 0u;
     const uint32_t ninc = wave_scan_add(ne);
-    // the carried segment: lane t < 16 tests its t-th candidate (cycle t >> 2, entry t & 3 of 257,
-    // 0, 1, 2 rotated to start at R0)
+    // the carried segment: lane t < 16 kQ tests its t-th candidate (cycle t >> 2, entry t & 3 of
+    // 257, 0, 1, 2 rotated to start at R0)
     const uint32_t rot = R0 <= 2 ? R0 + 1 : 0u;
     const uint32_t q = (lane + rot) & 3u;
     const uint32_t e = q == 0 ? 257u : q - 1u;
     const uint32_t ic = mod258(e + 258u - R0) + 258u * (lane >> 2);
-    const uint32_t nc = (uint32_t)__builtin_popcountll(ballot(lane < 16 && ic < p0));
+    const uint32_t nc = (uint32_t)__builtin_popcountll(ballot(lane < 16 * kQ && ic < p0));
     const uint32_t total = nc + lane_read(ninc, 63);
     if (total > 63) return kDense;
     // markers: each start's key (its first symbol's index, count flag and value, run byte) at row
@@ -1120,9 +1132,9 @@ __device__ __forceinline__ uint32_t rle_block(const u32x4 x, RleCarry &cy, uint8
     *(lane < total ? sb + at + lane : reinterpret_cast<uint8_t *>(row + 63)) = (uint8_t)v;
     __builtin_amdgcn_wave_barrier();
     // carries: the block's last raw and diffed byte, the run counter after it
-    cy.x = lane_read(x[3], 63) >> 24;
-    cy.c = lane_read(c[3], 63) >> 24;
-    cy.R = mod258(S ? 1024u - lane_read(p, S - 1) : R0 + 1024u);
+    cy.x = lane_read(x[kX - 1], 63) >> 24;
+    cy.c = lane_read(c[kX - 1], 63) >> 24;
+    cy.R = mod258(S ? kBytes - lane_read(p, S - 1) : R0 + kBytes);
     return at + total;
 }
 
@@ -1715,13 +1727,19 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         uint32_t chunk = 0;
         bool redo = false;     // the chunk did not fit the pending symbols: again, after coding them
         // Run-heavy stretches (a 256-byte chunk whose run starts sit in at most kSparseEnter
-        // lanes) switch to 1 KB blocks coded by segments (rle_block; tests/rle_chunk_model.py:
-        // rle_blocked) while the blocks stay sparse and four full chunks remain before the last
-        // one; blk holds the block at ci (one 16-byte load per lane, the next one in flight).
+        // lanes) switch to blocks of kQ KB coded by segments (rle_block; tests/rle_chunk_model.py:
+        // rle_blocked) while the blocks stay sparse and a whole block of full chunks remains before
+        // the last one; blk holds the block at ci (kQ 16-byte loads per lane, the next block in
+        // flight).
         constexpr bool kSparseOn = HC_SPARSE && !kWin && kSrc != SRC_SYMBOLS && !kTab;
         constexpr uint32_t kSparseEnter = 2;
+        constexpr uint32_t kQ = HC_SPARSE_KB, kBC = 4 * kQ;  // KB and 256-byte chunks per block
         bool sparse = false;
-        u32x4 blk = {0u, 0u, 0u, 0u};
+        u32x4 blk[kQ] = {};
+        auto load_blk = [&](uint32_t c0) __attribute__((always_inline)) {
+#pragma unroll
+            for (uint32_t i = 0; i < kQ; ++i) blk[i] = buf_load4(rin, 256 * c0 + 16 * (kQ * lane + i));
+        };
         for (uint32_t ci = 0;;) {
             const bool more = ci < nch && !fgk.bad;
             uint32_t full = 0;
@@ -1731,15 +1749,15 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                 } else {
                     prio.at(ci, nch);
                     HC_PROF_BEGIN();
-                    const uint32_t r = rle_block<kSrc>(blk, cy, sb_w, np, fgk.T.scratch, lane);
+                    const uint32_t r = rle_block<kSrc, kQ>(blk, cy, sb_w, np, fgk.T.scratch, lane);
                     HC_PROF_END(4);
                     if (r != kDense) {
                         np = r;
-                        ci += 4;
+                        ci += kBC;
                         full = np + 63 > kSymWords * 4 ? 1u : 0u;
                     }
-                    if (r != kDense && ci + 4 < nch) {
-                        blk = buf_load4(rin, 256 * ci + 16 * lane);
+                    if (r != kDense && ci + kBC < nch) {
+                        load_blk(ci);
                     } else {  // a dense block or the last chunks: 256-byte chunks from ci
                         sparse = false;
                         next = buf_load(rin, 256 * ci + lane * 4);
@@ -1779,9 +1797,9 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                     np = rle_chunk<kSrc>(chunk, m, ci + 1 == nch ? 1u : 0u, cy, sb_w, np, kWin ? 342u : kSymWords * 4,
                                          fgk.scr32(), lane, full, slanes);
                     HC_PROF_END(4);
-                    if (kSparseOn && !full && slanes <= kSparseEnter && ci + 5 < nch) {
+                    if (kSparseOn && !full && slanes <= kSparseEnter && ci + 1 + kBC < nch) {
                         sparse = true;  // the block at ci + 1 (the chunk loaded ahead is dropped)
-                        blk = buf_load4(rin, 256 * (ci + 1) + 16 * lane);
+                        load_blk(ci + 1);
                     }
                     if (kWin) {
                         full = !full;  // code this chunk's symbols now (the chunk itself always fits)

@@ -79,9 +79,9 @@ def pure_chunk(R, c):
     return bytes(out), (R + 256) % 258
 
 
-# ---- 1 KB blocks for run-heavy streams (hc_fgk.hip: rle_block) ----------------------------
+# ---- 2 KB blocks for run-heavy streams (hc_fgk.hip: rle_block, HC_SPARSE_KB) --------------
 #
-# A full, non-final 1 KB block with few run starts (<= kSparseStarts) is coded by segments instead
+# A full, non-final block (kBlock bytes: 2 KB as the kernel, 1 KB its other build) with few run starts (<= kSparseStarts) is coded by segments instead
 # of byte by byte. Its bytes split at the run starts p_0 < .. < p_{S-1}: the carried segment
 # [0, p_0) continues the run before the block (byte i at k = R + i, R the carried run counter) and
 # segment j = [p_j, p_{j+1}) is a new run (k = i - p_j). Per byte, with km = k mod 258:
@@ -92,7 +92,7 @@ def pure_chunk(R, c):
 # residues 0, 1, 2, 257, 258 = 0, ...); the carried segment's start at residue R instead. The run
 # counter before start j is (R + p_0) mod 258 for j = 0 and L_{j-1} mod 258 after a new run of
 # length L_{j-1}. The kernel gives each start a lane and each event a lane (<= 63 events).
-kBlock = 1024
+kBlock = 2048
 kSparseStarts = 16
 
 
@@ -107,7 +107,7 @@ def carried_events(R, L):
     cycle t >> 2, entry t & 3 of the cyclic order 257, 0, 1, 2 rotated to start at R)"""
     rot = R + 1 if R <= 2 else 0
     out = []
-    for t in range(16):
+    for t in range(16 * kBlock // 1024):  # (the kernel's lanes t < 16 kQ)
         q = (t + rot) & 3
         e = 257 if q == 0 else q - 1
         i = (e - R) % 258 + 258 * (t >> 2)
@@ -117,9 +117,9 @@ def carried_events(R, L):
 
 
 def sparse_block(c, c_carry, R):
-    """c: the block's 1024 diffed bytes. Returns (symbols, R after the block), or None when the
+    """c: the block's kBlock diffed bytes. Returns (symbols, R after the block), or None when the
     block has more than kSparseStarts starts or more than 63 symbols (the kernel then codes it as
-    four 256-byte chunks)."""
+    256-byte chunks)."""
     c = np.asarray(c, dtype=np.int64)
     prev = np.concatenate([[c_carry], c[:-1]])
     start = c != prev
@@ -146,8 +146,9 @@ def sparse_block(c, c_carry, R):
 def rle_blocked(data, diff=False):
     """The kernel's chunk loop for a stream that fits one buffer window: 256-byte chunks
     (rle_chunked's per-chunk rule) until a chunk has at most kSparseEnter starting lanes, then
-    1 KB blocks while they are sparse and four full chunks remain before the last one; a dense
-    block goes back to 256-byte chunks."""
+    blocks of kBlock bytes while they are sparse and a whole block of full chunks remains before
+    the last one; a dense block goes back to 256-byte chunks."""
+    kb = kBlock // 256
     data = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.int64)
     n = data.size
     nch = (n + 255) // 256
@@ -160,7 +161,7 @@ def rle_blocked(data, diff=False):
         return (x - xp) & 255 if diff else x.copy()
 
     while ci < nch:
-        if sparse and ci + 4 < nch:
+        if sparse and ci + kb < nch:
             x = data[256 * ci:256 * ci + kBlock]
             c = diffed(x, prev_x)
             r = sparse_block(c, c_carry, R_carry)
@@ -168,7 +169,7 @@ def rle_blocked(data, diff=False):
                 sym, R_carry = r
                 out += list(sym)
                 prev_x, c_carry = int(x[-1]), int(c[-1])
-                ci += 4
+                ci += kb
                 continue
             sparse = False
         base = 256 * ci

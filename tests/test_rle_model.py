@@ -2,6 +2,7 @@
 (tests/rle_chunk_model.py), equals the reference's serial FSM (oracle, transform.cpp:241-279)
 on run structures around every 258-byte cut and 256-byte chunk boundary."""
 import numpy as np
+import pytest
 
 from rle_chunk_model import rle_chunked
 
@@ -85,11 +86,15 @@ def _run_heavy(rng, n):
     return b"".join(parts)[:n]
 
 
-def test_blocked_rle_equals_serial(oracle_mod):
-    """the encoder's 1 KB sparse blocks (rle_chunk_model.rle_blocked, hc_fgk.hip rle_block) inside
-    the chunk loop equal the reference's FSM (transform.cpp:241-279): run-heavy streams with dense
-    stretches, every carried counter phase, both diff settings, and the grad photos"""
+@pytest.mark.parametrize("block", [2048, 1024])
+def test_blocked_rle_equals_serial(oracle_mod, block, monkeypatch):
+    """the encoder's sparse blocks (rle_chunk_model.rle_blocked, hc_fgk.hip rle_block; 2 KB as
+    shipped, 1 KB the HC_SPARSE_KB=1 build) inside the chunk loop equal the reference's FSM
+    (transform.cpp:241-279): run-heavy streams with dense stretches, every carried counter phase,
+    both diff settings, and the grad photos"""
+    import rle_chunk_model
     from rle_chunk_model import rle_blocked
+    monkeypatch.setattr(rle_chunk_model, "kBlock", block)
     rng = np.random.default_rng(5)
     for t in range(160):
         data = _run_heavy(rng, int(rng.integers(1, 24000)))
