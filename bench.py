@@ -1,25 +1,33 @@
 #!/usr/bin/env python3
 """bench.py — encode+decode GiB/s of the MI355X huffman-codec on batched 512x512 .raw streams.
 
-Headline workload = BASELINE.json configs[4] (C5): a batch of 65536 synthetic 512x512 photo
-streams (seed 0x5EED, generated in HBM) per GPU. The streams are
-independent units, so N GPUs code N such batches, one per rank, with no data-path collective
-(weak scaling, per-GPU work fixed: rank r owns streams [r*S, (r+1)*S) of the global sequence, S =
-65536; at N=1 the GPU codes exactly the C5 batch). --total-streams T instead splits one batch of T
-streams over the ranks (strong scaling; T = 65536 is C5's batch spread over N GPUs: at N=8 each
-GPU then holds 8192 streams, a single round of wavefronts that ends with its slowest stream). One step is the reference's full round trip on the shard: `-c -m` encode
-(diff -> MNP-5 RLE -> FGK -> header, one fused kernel) then decode (FGK -> RLE revert -> diff
-revert, one fused kernel). value = raw bytes of all ranks / step time (max over ranks), GiB/s.
-After the timed region: every status 0, decode == input on every stream, and (rank 0, N=1) the
-first streams' encodings byte-identical to the reference binary's own output for them.
+Headline workload = BASELINE.json configs[4] (C5): ONE batch of 65536 synthetic 512x512 photo
+streams (seed 0x5EED, generated in HBM), split over the N GPUs (strong
+scaling, as BASELINE defines C5: rank r owns streams [r*S, (r+1)*S), S = 65536 / N; at N=8 each GPU
+holds 8192 streams). The streams are independent units, so there is no data-path collective.
+One step is the reference's full round trip on the shard: `-c -m` encode (diff -> MNP-5 RLE ->
+FGK -> header, one fused kernel) then decode (FGK -> RLE revert -> diff revert, one fused kernel).
+value = raw bytes of all ranks / step time (max over ranks), GiB/s. After the timed region: every
+status 0, decode == input on every stream, and (rank 0, N=1) the first streams' encodings
+byte-identical to the reference binary's own output for them.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`--gpus N` with N > 1 and no launcher around the process starts the N ranks itself (fresh child
+processes through torch.distributed.run, before anything here touches a GPU) and exits with their
+status; under a launcher, --gpus must equal WORLD_SIZE. At N > 1 the line also carries
+`weak_scaling`: every rank then codes a whole 65536-stream batch of its own (per-GPU work fixed),
+measured after the headline and reported beside it, never as `value`. `--weak` makes --streams a
+per-GPU count for the headline itself.
+
 At N=1 the same JSON line also carries "configs": the other BASELINE.json configs measured in
-the same run (C2 one stream, C3 4096 streams `-c`, C4 the 4096x4096 adaptive matrix, and the
-grad / noise distributions of SURVEY.md §8d), each checked against the reference's digests
-(tests/golden/digests.json) or by round trip, each with its own roofline line.
+the same run (C1 the per-file CLI, C2 one stream, C3 4096 streams `-c`, C4 the 4096x4096
+adaptive matrix, the grad / noise distributions of SURVEY.md §8d, and C5_split2/4/8: the shard
+one GPU holds when C5 is split over 2 / 4 / 8 GPUs, with its efficiency against the whole batch),
+each checked against the reference's digests (tests/golden/digests.json) or by round trip. The
+full per-config record (rooflines, adaptive stages, CLI phases) is printed first on a line of its
+own starting with "detail "; the last line is the one JSON result.
 
 Streams are independent, so ranks share nothing on the data path; after the timed region RCCL
 all-reduces the verification counters and the max step time.
@@ -53,9 +61,11 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--streams", type=int, default=C5_STREAMS, help="streams per GPU (weak scaling)")
-    ap.add_argument("--total-streams", type=int, default=0,
-                    help="strong scaling instead: streams in the whole batch, split over the ranks")
+    ap.add_argument("--streams", "--total-streams", dest="streams", type=int, default=C5_STREAMS,
+                    help="streams in the whole batch, split over the ranks (strong scaling; 65536 = C5)")
+    ap.add_argument("--weak", action="store_true", help="--streams per GPU instead (weak scaling)")
+    ap.add_argument("--no-weak-line", action="store_true",
+                    help="N > 1: skip the extra weak-scaling measurement (a whole C5 batch per GPU)")
     ap.add_argument("--kind", default="photo", choices=["photo", "grad", "noise"])
     ap.add_argument("--no-diff", action="store_true", help="-c instead of -c -m")
     ap.add_argument("--cpu-sample", type=int, default=0, help="streams for the CPU baseline (0 = auto)")
@@ -484,6 +494,14 @@ def config_mixed(torch, hc, dev, stream, photos=6144, noises=2048):
 
 
 CLI_BIN = os.path.join(ROOT, "huffman-codec_amd", "bin", "huffman-codec")
+FLOOR_BIN = os.path.join(ROOT, "huffman-codec_amd", "bin", "hc-floor")
+
+
+def _hc_times(stderr):
+    for line in stderr.decode(errors="replace").splitlines():
+        if line.startswith("hc-times "):
+            return {k: float(v) for k, v in (f.split("=") for f in line.split()[1:])}
+    return None
 
 
 def config_cli(reps=7):
@@ -492,12 +510,17 @@ def config_cli(reps=7):
     its start, for this repo's GPU CLI and for the reference binary (oracle/_ref, -O2 and the
     Makefile's -O0), median of `reps` runs each. hd01.raw is recovered on the box by decoding the
     reference's committed output tests/golden/corpus/hd01.cm.huf with the reference binary; every
-    binary's .huf must equal that file and every decode must give hd01.raw back. The GPU CLI also
-    reports its in-process phases (HC_CLI_TIMES=1: read, HIP start-up, coding, write), so its wall
-    time splits into process start + library load, HIP start-up and coding, and the coding into its
-    one-time part (code objects loaded at the first launch, first allocations) and the rest
-    (code_again_ms: the same call repeated in the process, i.e. copies in and out plus kernels).
-    The phase runs are separate from the wall-clock runs (they code twice)."""
+    binary's .huf must equal that file and every decode must give hd01.raw back.
+
+    The floor: bin/hc-floor, an empty HIP program (process start, HIP start-up, one empty kernel
+    launched and waited for) timed the same way on the same box; `cli_minus_floor_ms` is what the
+    CLI costs per file above what any GPU process costs. The GPU CLI also reports its in-process
+    phases (HC_CLI_TIMES=1: read, HIP start-up, coding, write), so its wall time splits into process
+    start + library load, HIP start-up and coding, and the coding into its one-time part (code
+    objects loaded at the first launch, first allocations) and the rest (code_again_ms: the same
+    call repeated in the process, i.e. copies in and out plus kernels). The phase runs are separate
+    from the wall-clock runs (they code twice). A failing binary is recorded in the entry (and
+    counted bad) instead of aborting the other configs."""
     import statistics
     import subprocess
 
@@ -511,18 +534,45 @@ def config_cli(reps=7):
     want = open(golden, "rb").read()
     tmp = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
     bad = 0
+    out = {"what": "C1: hd01.raw -c -m then -d, one process per file (the reference's use case), "
+                   f"median of {reps} runs, wall clock including process start", "binaries": {}}
     try:
-        subprocess.run([ref, "-d", "-i", golden, "-o", "hd01.raw"], cwd=tmp, check=True, capture_output=True)
+        r = subprocess.run([ref, "-d", "-i", golden, "-o", "hd01.raw"], cwd=tmp, capture_output=True)
+        if r.returncode != 0:
+            out["error"] = f"reference decode of hd01.cm.huf: exit {r.returncode}"
+            return out, 1
         raw = open(os.path.join(tmp, "hd01.raw"), "rb").read()
-        out = {"what": "C1: hd01.raw -c -m then -d, one process per file (the reference's use case), "
-                       f"median of {reps} runs, wall clock including process start",
-               "file_bytes": len(raw), "binaries": {}}
+        out["file_bytes"] = len(raw)
+        if os.path.exists(FLOOR_BIN):
+            walls, phases, err = [], [], None
+            for rep in range(2 * reps):
+                timing = rep >= reps
+                env = dict(os.environ, HC_CLI_TIMES="1") if timing else None
+                t0 = time.perf_counter()
+                r = subprocess.run([FLOOR_BIN], cwd=tmp, capture_output=True, env=env)
+                if r.returncode != 0:
+                    err = f"exit {r.returncode}: {r.stderr[-200:]!r}"
+                    break
+                if timing:
+                    p = _hc_times(r.stderr)
+                    if p:
+                        phases.append(p)
+                else:
+                    walls.append(time.perf_counter() - t0)
+            if err:
+                out["floor"] = {"error": err}
+            else:
+                fl = {"binary": os.path.relpath(FLOOR_BIN, ROOT), "wall_s": round(statistics.median(walls), 4)}
+                if phases:
+                    fl["phases_ms"] = {k: round(statistics.median(p[k] for p in phases), 3) for k in phases[0]}
+                out["floor"] = fl
         legs = [("gpu_cli", CLI_BIN), ("reference_O2", oracle.REF_BIN_O2), ("reference_O0", oracle.REF_BIN)]
         for label, binary in legs:
             if not os.path.exists(binary):
                 continue
             enc_t, dec_t, phases = [], [], {"encode": [], "decode": []}
             same = rt = True
+            err = None
             for rep in range(2 * reps if label == "gpu_cli" else reps):
                 timing = rep >= reps  # the GPU CLI's phase runs come after its wall-clock runs
                 env = dict(os.environ, HC_CLI_TIMES="1") if timing else None
@@ -533,12 +583,19 @@ def config_cli(reps=7):
                     if not timing:
                         t.append(time.perf_counter() - t0)
                     if r.returncode != 0:
-                        raise RuntimeError(f"C1 {label} {d}: exit {r.returncode}: {r.stderr[-300:]!r}")
-                    for line in r.stderr.decode(errors="replace").splitlines():
-                        if line.startswith("hc-times "):
-                            phases[d].append({k: float(v) for k, v in (f.split("=") for f in line.split()[1:])})
+                        err = f"{d}: exit {r.returncode}: {r.stderr[-300:]!r}"
+                        break
+                    p = _hc_times(r.stderr)
+                    if p:
+                        phases[d].append(p)
+                if err:
+                    break
                 same &= open(os.path.join(tmp, f"{label}.huf"), "rb").read() == want
                 rt &= open(os.path.join(tmp, f"{label}.out"), "rb").read() == raw
+            if err:
+                out["binaries"][label] = {"binary": os.path.relpath(binary, ROOT), "error": err}
+                bad += 1
+                continue
             leg = {"binary": os.path.relpath(binary, ROOT), "encode_s": round(statistics.median(enc_t), 4),
                    "decode_s": round(statistics.median(dec_t), 4), "encode_bytes_identical_to_reference": bool(same),
                    "round_trip": bool(rt)}
@@ -552,9 +609,16 @@ def config_cli(reps=7):
             out["binaries"][label] = leg
             bad += 0 if (same and rt) else 1
         g, r2 = out["binaries"].get("gpu_cli"), out["binaries"].get("reference_O2")
-        if g and r2:
+        if g and r2 and "encode_s" in g and "encode_s" in r2:
             out["gpu_over_reference_O2"] = {"encode": round(g["encode_s"] / r2["encode_s"], 3),
                                             "decode": round(g["decode_s"] / r2["decode_s"], 3)}
+        fl = out.get("floor", {})
+        if g and "encode_s" in g and "wall_s" in fl:
+            out["cli_minus_floor_ms"] = {"encode": round((g["encode_s"] - fl["wall_s"]) * 1e3, 1),
+                                         "decode": round((g["decode_s"] - fl["wall_s"]) * 1e3, 1)}
+    except (OSError, subprocess.SubprocessError) as e:
+        out["error"] = repr(e)[:300]
+        bad += 1
     finally:
         for fn in os.listdir(tmp):
             os.remove(os.path.join(tmp, fn))
@@ -562,7 +626,7 @@ def config_cli(reps=7):
     return out, bad
 
 
-def run_configs(torch, hc, dev, stream, only):
+def run_configs(torch, hc, dev, stream, only, c5_kernel_GiBps=None):
     with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
         digests = json.load(f)
     plan = [
@@ -571,6 +635,12 @@ def run_configs(torch, hc, dev, stream, only):
         ("grad", "8192 x 512x512 grad -c -m (best case: runs collapse the symbols)", "grad", 8192, True, 3),
         ("noise", "2048 x 512x512 noise -c -m (worst case: ~262k deep codes per stream)", "noise", 2048, True, 2),
     ]
+    # C5 split over 2 / 4 / 8 GPUs: the shard each GPU holds, coded here on one GPU. Its kernel
+    # throughput over the whole batch's is the strong-scaling efficiency ceiling at that N (the
+    # shards are independent; what one GPU does with 65536 / N streams is what each of N does)
+    for n in (2, 4, 8):
+        plan.append((f"C5_split{n}", f"{C5_STREAMS // n} x 512x512 photo -c -m: the shard of one GPU when C5 is "
+                                     f"split over {n} GPUs", "photo", C5_STREAMS // n, True, 3))
     res, bad = {}, 0
     if not only or "C1" in only:
         res["C1"], bad = config_cli()
@@ -578,6 +648,9 @@ def run_configs(torch, hc, dev, stream, only):
         if only and name not in only:
             continue
         res[name], b = config_batch(torch, hc, dev, stream, name, what, kind, S, d, steps, digests)
+        if name.startswith("C5_split") and c5_kernel_GiBps:
+            res[name]["kernel_GiBps_C5"] = round(c5_kernel_GiBps, 4)
+            res[name]["efficiency_vs_C5"] = round(res[name]["GiBps"] / c5_kernel_GiBps, 4)
         bad += b
     if not only or "mixed" in only:
         res["mixed"], b = config_mixed(torch, hc, dev, stream)
@@ -691,8 +764,103 @@ def time_gather(torch, hcdist, b, dev, barrier):
     return out
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 and no launcher around this process: start the N ranks (one per GPU) as fresh
+    child processes through torch.distributed.run, rendezvous on 127.0.0.1, before anything in this
+    process touches a GPU (no hcodec import, no HIP call: the children start from scratch); their
+    output passes straight through and their exit status is returned. Under a launcher (WORLD_SIZE
+    set) --gpus must equal the launcher's world size: a mismatch exits non-zero instead of measuring
+    some other number of GPUs. Returns None when this process is itself the (only) rank."""
+    import subprocess
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr, flush=True)
+            raise SystemExit(2)
+        return None
+    if args.gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def workload_name(total, world, S, kind, use_diff, weak):
+    mode = "-c -m" if use_diff else "-c"
+    how = (f"{S} per GPU, weak scaling" if weak else f"split over {world} GPU(s), {S} per GPU")
+    c5 = total == C5_STREAMS and not weak and kind == "photo" and use_diff
+    return (f"{'C5: ' if c5 else ''}{total} x 512x512 {kind} streams ({how}), {mode} encode + decode round trip")
+
+
+def weak_line(torch, hc, hcdist, args, dev, stream, rank, world, barrier, dry, use_diff, N):
+    """N > 1: every rank codes a whole batch of its own (C5's 65536 streams; the dry run: --streams),
+    streams k = r*S .. r*S + S - 1, timed like the headline (max over ranks), verified the same way.
+    Per-GPU work fixed: the weak-scaling figure, reported beside `value`, never as it."""
+    S = args.streams if dry else C5_STREAMS
+    steps = max(1, min(args.steps, 3))
+    b = StandInBatch(torch, rank * S, S, N) if dry else Batch(torch, hc, dev, args.kind, rank * S, S, use_diff)
+    wall, enc_ms, dec_ms = timed(torch, b, stream, steps, 1, barrier)
+    bad = b.bad()
+    del b
+    if not dry:
+        torch.cuda.empty_cache()
+    elapsed = float(hcdist.reduce_counters([wall], op="max", device=dev)[0])
+    bad = int(hcdist.reduce_counters([bad], device=dev)[0])
+    if bad:
+        raise SystemExit(f"weak-scaling pass: bit-exact check FAILED on {bad} items")
+    step_s = elapsed / steps
+    return {"what": "every rank codes a whole batch of its own (per-GPU work fixed); beside value, not value",
+            "scaling": "weak", "streams_per_gpu": S, "streams_total": world * S, "steps": steps,
+            "ms_per_step": round(step_s * 1e3, 3), "value": round(world * S * N / step_s / 2**30, 4),
+            "unit": "GiB/s", "bit_exact": True}
+
+
+# keys of a config's record kept in the final JSON line (the full record goes on the "detail" line)
+_KEEP = ("streams", "mode", "kind", "encode_ms", "decode_ms", "GiBps", "round_trip_exact",
+         "reference_digests_identical", "fgk_symbols_per_stream", "efficiency_vs_C5",
+         "kernel_GiBps_C5", "encode_mixed_over_parts", "skipped")
+
+
+def compact_configs(configs):
+    out = {}
+    for name, c in configs.items():
+        d = {k: c[k] for k in _KEEP if k in c}
+        if isinstance(c.get("roofline"), dict):
+            d["hbm_frac"] = c["roofline"].get("frac")
+        if isinstance(c.get("issue"), dict):
+            d["issue_frac"] = c["issue"].get("frac")
+        st = c.get("stages")
+        if isinstance(st, dict):
+            d["stages_ms"] = {k: v["ms"] for part in ("encode", "decode") for k, v in st.get(part, {}).items()
+                              if k in ("tile_cost", "emit_tile", "unblock_tile", "block_boundaries", "undiff",
+                                       "fgk_encode", "fgk_decode")}
+        if name == "C1":
+            for k in ("floor", "cli_minus_floor_ms", "gpu_over_reference_O2", "error"):
+                if k in c:
+                    d[k] = c[k]
+            d["binaries"] = {b: {k: v[k] for k in ("encode_s", "decode_s", "encode_bytes_identical_to_reference",
+                                                    "round_trip") if k in v}
+                             for b, v in c.get("binaries", {}).items()}
+        out[name] = d
+    return out
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    rc = launch_ranks(args, argv)
+    if rc is not None:
+        raise SystemExit(rc)
     import torch
     import torch.distributed as dist
     import hcdist
@@ -723,10 +891,12 @@ def main(argv=None):
         print(json.dumps({"configs": res, "bad": bad}), flush=True)
         raise SystemExit(1 if bad else 0)
 
-    strong = args.total_streams > 0
-    if strong and args.total_streams % world:
-        raise SystemExit(f"--total-streams {args.total_streams} does not split over {world} ranks")
-    S = args.total_streams // world if strong else args.streams
+    if args.weak:
+        S = args.streams
+    else:
+        if args.streams % world:
+            raise SystemExit(f"--streams {args.streams} does not split over {world} ranks")
+        S = args.streams // world
     total = world * S
     use_diff = not args.no_diff
     N = args.dry_stream_bytes if dry else N_RAW
@@ -750,10 +920,9 @@ def main(argv=None):
     result = {
         "metric": METRIC, "value": round(value, 4), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
-        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8",
+        "higher_is_better": True, "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "u8",
         "data": f"synthetic {args.kind} (SURVEY.md App. D, seed 0x5EED), generated in HBM",
-        "config": {"workload": f"C5: {total} x 512x512 {args.kind} streams over {world} GPU(s) "
-                               f"({S} per GPU), {'-c -m' if use_diff else '-c'} encode + decode round trip",
+        "config": {"workload": workload_name(total, world, S, args.kind, use_diff, args.weak),
                    "streams_total": total, "streams_per_gpu": S, "stream_bytes": N,
                    "mode": "-c -m" if use_diff else "-c",
                    "parallelism": f"dp{world} (stream shards, no data-path collective)"},
@@ -762,7 +931,7 @@ def main(argv=None):
         "encode_GiBps": round(world * S * N / (enc_ms * 1e-3) / 2**30, 4) if enc_ms > 0 else None,
         "decode_GiBps": round(world * S * N / (dec_ms * 1e-3) / 2**30, 4) if dec_ms > 0 else None,
         "bits_per_byte": round(enc_total * 8 / raw_total, 4), "bit_exact": True,
-        "fgk_symbols_per_stream": round(b.fgk_symbols() / S, 1),
+        "fgk_symbols_per_stream": round(b.fgk_symbols() / S, 1) if S else None,
     }
     if dry:
         result.update({"metric": METRIC + " [gloo dry run: streams copied, not coded]", "dry_run": True,
@@ -793,12 +962,20 @@ def main(argv=None):
             result["cpu_baseline"] = cb
             result["bit_exact_vs_reference_streams"] = sample
     del b
-    cbad = 0
     if not dry:
         torch.cuda.empty_cache()
-        if world == 1 and not args.no_configs:
-            result["configs"], cbad = run_configs(torch, hc, dev, stream, set())
-            result["configs_bit_exact"] = cbad == 0
+    if world > 1 and not args.no_weak_line:
+        result["weak_scaling"] = weak_line(torch, hc, hcdist, args, dev, stream, rank, world, barrier, dry,
+                                           use_diff, N)
+    cbad = 0
+    if not dry and world == 1 and not args.no_configs:
+        c5_kernel = S * N / ((enc_ms + dec_ms) * 1e-3) / 2**30 if S == C5_STREAMS and use_diff and \
+            args.kind == "photo" else None
+        configs, cbad = run_configs(torch, hc, dev, stream, set(), c5_kernel)
+        result["configs_bit_exact"] = cbad == 0
+        if rank == 0:
+            print("detail " + json.dumps({"configs": configs}), flush=True)
+        result["configs"] = compact_configs(configs)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist.is_initialized():

@@ -1034,6 +1034,9 @@ __device__ __forceinline__ uint32_t rle_chunk(uint32_t x4, uint32_t m, uint32_t 
 #ifndef HC_SPARSE_KB
 #define HC_SPARSE_KB 2
 #endif
+// rle_block's start mask is 32 bits (one per run start slot), its positions stay below 2048 and
+// mod258's exactness bound (v < 2321) holds only up to 2 KB blocks
+static_assert(HC_SPARSE_KB == 1 || HC_SPARSE_KB == 2, "rle_block supports 1 KB and 2 KB sparse blocks only");
 constexpr uint32_t kSparseStarts = 16;
 constexpr uint32_t kDense = 0xFFFFFFFFu;
 template <int kSrc, uint32_t kQ>

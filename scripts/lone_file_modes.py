@@ -1,7 +1,8 @@
 """Single-buffer API (the CLI's path) on one real file, per encoder mode (diagnostic; debug build):
 encode and decode wall time of hc_compress / hc_decompress in a warm process, median of 7.
 
-    python scripts/lone_file_modes.py abvar/hd01.raw [--no-diff]
+    python scripts/lone_file_modes.py FILE.raw [--no-diff]
+    (hd01.raw: decode tests/golden/corpus/hd01.cm.huf with the reference binary first, as bench.py's C1 does)
 """
 import argparse
 import os

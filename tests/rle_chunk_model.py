@@ -143,11 +143,12 @@ def sparse_block(c, c_carry, R):
     return bytes(syms), Rn
 
 
-def rle_blocked(data, diff=False):
+def rle_blocked(data, diff=False, blocks=None):
     """The kernel's chunk loop for a stream that fits one buffer window: 256-byte chunks
     (rle_chunked's per-chunk rule) until a chunk has at most kSparseEnter starting lanes, then
     blocks of kBlock bytes while they are sparse and a whole block of full chunks remains before
-    the last one; a dense block goes back to 256-byte chunks."""
+    the last one; a dense block goes back to 256-byte chunks. `blocks`, when a list, receives
+    (byte offset, carried run counter R) of every block coded sparse."""
     kb = kBlock // 256
     data = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.int64)
     n = data.size
@@ -166,6 +167,8 @@ def rle_blocked(data, diff=False):
             c = diffed(x, prev_x)
             r = sparse_block(c, c_carry, R_carry)
             if r is not None:
+                if blocks is not None:
+                    blocks.append((256 * ci, R_carry))
                 sym, R_carry = r
                 out += list(sym)
                 prev_x, c_carry = int(x[-1]), int(c[-1])

@@ -97,39 +97,88 @@ def test_pack_single_process():
     assert hcdist.pack(buf, offs, lens).tolist() == [0, 1, 2, 30, 31, 32, 33, 34]
 
 
-@pytest.mark.parametrize("world,strong", [(1, False), (2, False), (3, False), (2, True)])
-def test_bench_multi_rank_dry_run(world, strong):
-    """bench.py's own multi-rank path (shards, barriers, max-over-ranks timing, counter reduction,
-    --gather) end to end under the driver's launcher, on CPU: --backend gloo swaps each rank's GPU
-    step for a stand-in that copies its streams. Rank 0 prints exactly one JSON line; the gathered
-    payload is every rank's shard in global stream order. Weak scaling (the headline: --streams per
-    GPU) and strong scaling (--total-streams split over the ranks) shard the same way."""
+def _check_dry_line(stdout, world, S, per, weak, N, weak_per):
     import hashlib
     import json
-    import subprocess
     import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    root = os.path.dirname(here)
-    S, N = 2 * world, 3000
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--backend", "gloo", "--gpus", str(world), "--steps", "3", "--warmup", "1",
-           "--gather", "--dry-stream-bytes", str(N)] + (["--total-streams", str(S)] if strong else ["--streams", "2"])
-    env = dict(os.environ, OMP_NUM_THREADS="1")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
-    assert p.returncode == 0, p.stderr[-3000:]
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
     r = json.loads(lines[0])
     assert r["dry_run"] is True and r["n_gpus"] == world and r["steps"] == 3 and r["warmup"] == 1
     # the launcher's process group exists at world 1 too (the RCCL path on a one-GPU box)
     assert r["process_group"] == {"backend": "gloo", "world": world}
-    assert r["config"]["streams_total"] == S and r["config"]["streams_per_gpu"] == 2
-    assert r["value"] > 0 and r["ms_per_step"] > 0 and r["scaling"] == ("strong" if strong else "weak")
+    assert r["config"]["streams_total"] == S and r["config"]["streams_per_gpu"] == per
+    assert r["value"] > 0 and r["ms_per_step"] > 0 and r["scaling"] == ("weak" if weak else "strong")
     assert r["bits_per_byte"] == 8.0  # the stand-in copies: encoded = raw bytes
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
     sys.path.insert(0, root)
     import bench
     want = torch.cat([bench.stand_in_stream(torch, k, N) for k in range(S)]).numpy().tobytes()
     g = r["gather"]
     assert g["bytes_to_rank0"] == S * N and g["rank0_spot_check"] is True
     assert g["packed_sha256"] == hashlib.sha256(want).hexdigest()
+    if world > 1:  # the weak-scaling figure rides beside value, never as it (dry run: --streams per rank)
+        w = r["weak_scaling"]
+        assert w["scaling"] == "weak" and w["bit_exact"] is True and w["value"] > 0
+        assert w["streams_per_gpu"] == weak_per and w["streams_total"] == world * weak_per
+    else:
+        assert "weak_scaling" not in r
+    return r
+
+
+@pytest.mark.parametrize("world,weak", [(1, False), (2, False), (3, False), (2, True)])
+def test_bench_multi_rank_dry_run(world, weak):
+    """bench.py's own multi-rank path (shards, barriers, max-over-ranks timing, counter reduction,
+    --gather) end to end under the driver's launcher, on CPU: --backend gloo swaps each rank's GPU
+    step for a stand-in that copies its streams. Rank 0 prints exactly one JSON line; the gathered
+    payload is every rank's shard in global stream order. The headline splits --streams over the
+    ranks (strong scaling, C5 as BASELINE defines it); --weak makes it a per-GPU count."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    N = 3000
+    S = 2 * world
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--backend", "gloo", "--gpus", str(world), "--steps", "3", "--warmup", "1",
+           "--gather", "--dry-stream-bytes", str(N)] + (["--weak", "--streams", "2"] if weak else ["--total-streams", str(S)])
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    _check_dry_line(p.stdout, world, S, 2, weak, N, 2 if weak else S)
+
+
+def test_bench_gpus_flag_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with NO launcher around it (the form of the driver's bench
+    command) starts its two ranks itself: one JSON line with n_gpus 2 from a world-2 process group,
+    C5-style split of --total-streams over the ranks"""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    N, S = 2000, 6
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                              "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--backend", "gloo", "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--gather", "--dry-stream-bytes", str(N), "--total-streams", str(S)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = _check_dry_line(p.stdout, 2, S, S // 2, False, N, S)
+    assert r["n_gpus"] == 2 and r["process_group"]["world"] == 2
+
+
+def test_bench_gpus_flag_mismatch_exits_nonzero():
+    """under a launcher, --gpus must equal WORLD_SIZE: a mismatch measures nothing and exits
+    non-zero (before any process group or device is touched)"""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--backend", "gloo", "--gpus", "3"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert p.returncode != 0
+    assert "--gpus 3" in p.stderr and not [l for l in p.stdout.splitlines() if l.startswith("{")]

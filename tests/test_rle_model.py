@@ -108,3 +108,23 @@ def test_blocked_rle_equals_serial(oracle_mod, block, monkeypatch):
         raw = oracle_mod.synth("grad", k, 512, 64).tobytes()
         for diff in (False, True):
             assert rle_blocked(raw, diff) == oracle_mod.rle(oracle_mod.diff(raw) if diff else raw)
+
+
+def test_block_edge_vectors_cover_every_carried_phase(oracle_mod):
+    """the 2 KB block-edge vectors of tests/test_gpu_sparse.py (_edge_streams): in the model of the
+    kernel's loop every one of them codes the blocks at 256 + 2048 and 256 + 4096 sparse, the run
+    counter carried into the block at 256 + 4096 takes all 258 phases over the set, and the output
+    equals the reference's FSM in both diff settings"""
+    from rle_chunk_model import rle_blocked
+    from test_gpu_sparse import _edge_streams
+    phases = set()
+    for i, raw in enumerate(_edge_streams()):
+        for diff in (False, True):
+            if diff:
+                raw = np.cumsum(np.frombuffer(raw, dtype=np.uint8), dtype=np.uint64).astype(np.uint8).tobytes()
+            blocks = []
+            assert rle_blocked(raw, diff, blocks) == oracle_mod.rle(oracle_mod.diff(raw) if diff else raw), (i, diff)
+            at = dict(blocks)
+            assert 256 + 2048 in at and 256 + 4096 in at, (i, diff, blocks[:4])
+            phases.add(at[256 + 4096])
+    assert phases == set(range(258))
