@@ -96,12 +96,19 @@ __device__ __forceinline__ void trace_wave(uint32_t sid, uint64_t t0, uint32_t l
 // Diagnostic build (-DHC_PROF, scripts/path_prof.py): lane i of a per-wave accumulator sums the
 // s_memtime cycles spent in region i of the kernel; at the end lanes 0..7 go to g_trace[8 *
 // stream + i], lane 0 holding the wave's whole life. Absent from normal builds.
-#ifdef HC_PROF
+// -DHC_COUNT (with -DHC_PROF): the lanes count events instead (HC_CNT(i): lane i), e.g. the
+// batch steps, retests and symbols coded alone of the batched paths
+#if defined(HC_PROF) && !defined(HC_COUNT)
 #define HC_PROF_BEGIN() const uint64_t hc_p0_ = __builtin_amdgcn_s_memtime()
 #define HC_PROF_END(i) (pacc += lane == (i) ? __builtin_amdgcn_s_memtime() - hc_p0_ : 0)
 #else
 #define HC_PROF_BEGIN()
 #define HC_PROF_END(i)
+#endif
+#ifdef HC_COUNT
+#define HC_CNT(i) (pacc += lane == (i) ? 1 : 0)
+#else
+#define HC_CNT(i)
 #endif
 __device__ __forceinline__ void prof_store(uint32_t sid, uint64_t t0, uint64_t pacc, uint32_t lane)
 {
@@ -188,6 +195,15 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 #endif
 #ifndef HC_DEC_EXIT8
 #define HC_DEC_EXIT8 1
+#endif
+// 1: a batch whose first failing symbol's failure may be false (its test counts no earlier batch
+// symbol through the next position) is tested again from that symbol with the earlier ones
+// committed (code_all_batch, Dec::decode_batch; model: fgk_batch_model.retry_len)
+// (measured, grad / C5 / noise, ms: 1 with the plausibility test below, encode 1.50 -> 1.51 / +1 %
+// / +0.3 %, decode 1.64 -> 1.66 / +0.7 % / +1 %; 2, the miss test only: encode ±0 / +1.2 % / ±0,
+// decode -5.5 % / ±0 / +2 %: the retest's ~35-55 instructions cost what the restarts they save do)
+#ifndef HC_BATCH_RETRY
+#define HC_BATCH_RETRY 0
 #endif
 #ifndef HC_BATCH_YIELD
 #define HC_BATCH_YIELD 5
@@ -1518,6 +1534,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         uint32_t t = 0;
         while (t < ns) {
             if (sink.n > 64 - kBatch) sink.pack();
+            HC_CNT(1);
             const uint32_t jmax = min(kBatch, ns - t);
             const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + t));
             const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
@@ -1535,12 +1552,57 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
             const uint32_t wn = *(const lds_u32 *)(size_t)wa;
             // 2. the tests; 3. the increments from the first failing symbol on taken back
-            const uint64_t fm = (ballot(w1 < wn) & am) | ballot(pos == kMissPos);
-            const uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
+            const uint64_t missm = ballot(pos == kMissPos);
+            uint64_t fm = (ballot(w1 < wn) & am) | missm;
+            uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
             if (jf < jmax) {
                 const uint32_t vdec = sel(kL63, (jf - jmax) * kIncU, 0u - kIncU);
                 __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~groups9(jf), wa, scb),
                                        vdec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#if HC_BATCH_RETRY
+                // 4. retest in place (tests/fgk_batch_model.py retry_len). The failure of symbol jf
+                // may be false: its test counted no earlier batch symbol through the next position
+                // a + 1 (c1 = 0) and every later one through its own a. With the symbols before it
+                // committed and the ones from it on taken back, the words of a and a + 1 hold the
+                // exact counts of the earlier symbols, so the same tentative test run again on
+                // symbols jf.. is exact for jf unless a later symbol passes a, and stays
+                // conservative for the rest. Run when the failure can be false -- the first
+                // failing lane is no miss, jf > 0, and an earlier symbol holds a + 1 or a later
+                // one a (register compares) -- and again while it moves jf on. grad -c -m: the
+                // four-symbol alphabet's ties end a batch every ~4 symbols on c1 alone
+                // (slot-form model: 1034 batches + 523 symbols alone per stream -> 671 + 15).
+                uint32_t j0 = 0;
+                while (jf > j0) {
+                    const uint32_t fl = ff1(fm);
+                    if ((missm >> fl) & 1u) {
+                        HC_CNT(5);
+                        break;
+                    }
+                    const uint64_t gl = groups9(jf);
+#if HC_BATCH_RETRY == 1
+                    const uint32_t fa = lane_read(pos, fl);
+                    if (!((ballot(pos == fa + 1) & gl) | (ballot(pos == fa) & am & ~groups9(jf + 1)))) {
+                        HC_CNT(4);
+                        break;
+                    }
+#endif
+                    HC_CNT(3);
+                    const uint64_t am2 = am & ~gl;  // symbols jf.. and the root lane
+                    const uint32_t w1r = *(const lds_u32 *)(size_t)(wa + 4);
+                    __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am2, wa, scb),
+                                           sel(kL63, (jmax - jf) * kIncU, kIncU), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    const uint32_t wnr = *(const lds_u32 *)(size_t)wa;
+                    fm = (ballot(w1r < wnr) & am2) | missm;
+                    j0 = jf;
+                    jf = min(ff1(fm) / kLv, jmax);
+                    if (jf > j0) HC_CNT(6);
+                    if (jf == jmax) break;
+                    __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~groups9(jf), wa, scb),
+                                           sel(kL63, (jf - jmax) * kIncU, 0u - kIncU), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+#endif
             }
             const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
             // the code record 1 << d | bits (bit k: level k's parity, left = even) from two ballots:
@@ -1554,6 +1616,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             sink.n += jf;
             t += jf;
             if (jf < jmax) {  // symbol t: not cached, or a level reported: coded alone
+                HC_CNT(2);
                 if (sink.n == 64) sink.pack();
                 const uint32_t sym = uni(sb[t]);
                 const uint32_t ent = uni(fgk.T.where[sym]) >> 10;
@@ -2287,13 +2350,47 @@ struct Dec {
         constexpr uint64_t kLeafLanes = 0x0040201008040201ull & ((1ull << (kB * kG)) - 1);
         // (ff1 of no lane: 0xFFFFFFFF, above every batch)
         const uint32_t jn = ff1(ballot(b & kNotLeaf) & kLeafLanes) / kG;
-        const uint32_t jf = min(min(ff1(ballot(w1 < wn) & actm) / kG, jn), jmax);
-        if (jf < jmax)
+        uint64_t ft = ballot(w1 < wn) & actm;
+        uint32_t jf = min(min(ff1(ft) / kG, jn), jmax);
+        if (jf < jmax) {
             __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(actm & ~groups9(jf), wa, scr), 0u - kI,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#if HC_BATCH_RETRY
+            // 4. retest in place when the failure of symbol jf (a leaf) may be false, as the
+            // encoder's code_all_batch does: the symbols before it committed, the words of its a
+            // and a + 1 hold the earlier symbols' exact counts
+            uint32_t j0 = 0;
+            while (jf > j0 && jf < jn) {
+                const uint64_t gl = groups9(jf);
+#if HC_BATCH_RETRY == 1
+                const uint32_t fa = lane_read(pos, ff1(ft));
+                if (!((ballot(pos == fa + 1) & gl) | (ballot(pos == fa) & actm & ~groups9(jf + 1)))) {
+                    HC_CNT(4);
+                    break;
+                }
+#endif
+                HC_CNT(3);
+                const uint64_t am2 = actm & ~gl;  // symbols jf..
+                const uint32_t w1r = *(const lds_u32 *)(size_t)(wa + 4);
+                __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am2, wa, scr), kI, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WAVEFRONT);
+                const uint32_t wnr = *(const lds_u32 *)(size_t)wa;
+                ft = ballot(w1r < wnr) & am2;
+                j0 = jf;
+                jf = min(min(ff1(ft) / kG, jn), jmax);
+                if (jf > j0) HC_CNT(6);
+                if (jf == jmax) break;
+                __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(actm & ~groups9(jf), wa, scr), 0u - kI,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+#endif
+        }
         const uint32_t sb0 = (uint32_t)(size_t)(lds_u8 *)sbuf + (uint32_t)(i - i0);
         *(lds_u8 *)(size_t)sel(kLeafLanes & groups9(jf), sb0 + bj, scr) = (uint8_t)b;
         __builtin_amdgcn_wave_barrier();
+        HC_CNT(1);
+        if (jf < jmax) HC_CNT(2);
+        if (jf == jn && jf < jmax) HC_CNT(5);
         const uint32_t sj = lane_read(sv, jf);
         in.win = w0 << sj;
         in.nwin = n0 - sj;
