@@ -201,7 +201,9 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 // committed (code_all_batch, Dec::decode_batch; model: fgk_batch_model.retry_len)
 // (measured, grad / C5 / noise, ms: 1 with the plausibility test below, encode 1.50 -> 1.51 / +1 %
 // / +0.3 %, decode 1.64 -> 1.66 / +0.7 % / +1 %; 2, the miss test only: encode ±0 / +1.2 % / ±0,
-// decode -5.5 % / ±0 / +2 %: the retest's ~35-55 instructions cost what the restarts they save do)
+// decode -5.5 % / ±0 / +2 %: the retest's ~35-55 instructions cost what the restarts they save do;
+// the decoder's alone, in the blocks of streams that have seen <= 16 symbols (a second copy of the
+// block loop): grad decode -2.7 %, C5 decode +0.3 %, C3 decode +0.8 %)
 #ifndef HC_BATCH_RETRY
 #define HC_BATCH_RETRY 0
 #endif
