@@ -241,7 +241,7 @@ using WeightT = std::conditional_t<kW == 2, uint64_t, uint32_t>;
 // decoder each add their cache (tests/fgk_cache_model.py is the executable model of both,
 // checked against the plain slot form). kTab: the encoder's table mode (no path cache; the
 // decoder's level tables plus pcode[], ~6.5 KB, 6 waves per SIMD).
-template <int kW, bool kDec, bool kTab = false>
+template <int kW, bool kDec, bool kTab = false, bool kSmall = false>
 struct alignas(16) Tree {
     WeightT<kW> wt[kWords];           // narrow: weight << 10 | parent; wide / huge: weight
     uint32_t scratch[kW == 2 ? 128 : 64];  // landing words of lanes that must not write
@@ -267,6 +267,9 @@ struct alignas(16) Tree {
     // table mode: position -> its code as the level tables reached it: the prefix left-aligned
     // to 8 bits | (depth - 1) << 8 (checked against the tables at every use: stale entries fail)
     uint16_t pcode[kTab ? 516 : 2];
+    // the small-alphabet kernels (kSmall, narrow layout): the batch steps' membership marks (code_all_batch):
+    // bit 16 (a & 1) + j of word (a - 480) >> 1 says batch symbol j's path holds position a (480..513)
+    uint32_t smark[kSmall ? 17 : 1];
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // a byte in LDS (32-bit address)
@@ -407,7 +410,7 @@ __device__ __forceinline__ uint32_t wave_scan_add(uint32_t x)
 
 // ------------------------------------------------------------------------------ the tree --
 
-template <int kW, bool kDec, bool kTab = false>
+template <int kW, bool kDec, bool kTab = false, bool kSmall = false>
 struct Fgk {
     static constexpr bool kTabs = kDec || kTab;  // keeps the level tables
     static constexpr bool kWide = kW != 0;  // weights apart from parents (wide / huge)
@@ -415,7 +418,7 @@ struct Fgk {
     using Wt = WeightT<kW>;
     static constexpr Wt kInc = kWide ? 1u : 1024u;
 
-    Tree<kW, kDec, kTab> &T;
+    Tree<kW, kDec, kTab, kSmall> &T;
     uint32_t lane;
     uint32_t nyt;    // position of the NYT leaf: 512 - 2 * (symbols seen)
     uint32_t bad;    // a structural invariant broke (a bug, never valid input): stop, report
@@ -430,7 +433,7 @@ struct Fgk {
     const uint16_t *pc_lane;  // encoder: &pc[(lane & 15) - kRow]: where[] entry e's row (0: pc_miss)
     uint64_t pacc = 0;        // HC_PROF regions inside the tree code
 
-    __device__ __forceinline__ Fgk(Tree<kW, kDec, kTab> &t, uint32_t l)
+    __device__ __forceinline__ Fgk(Tree<kW, kDec, kTab, kSmall> &t, uint32_t l)
         : T(t), lane(l), nyt(kRoot), bad(0), pc_next(0), pc_free(0xFFFFu), pc_lb(0), pc_lb_ok(0), gen(0), stale(0), from(0),
           pc_lane(&t.pc[0] + (l & 15u) - (kTabs ? 0 : kRow))
     {
@@ -447,6 +450,7 @@ struct Fgk {
         }
         if (!kDec) {
             for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
+            if (kSmall && lane < sizeof(T.smark) / 4) T.smark[lane] = 0;
             if constexpr (kTab) {
                 for (uint32_t i = lane; i < 516; i += 64) T.pcode[i] = 0;
             } else {
@@ -1269,7 +1273,9 @@ constexpr int kWavesPerSimd = kTab ? (kW == 0 ? 6 : 5) : (kW == 0 ? HC_WPE0 : (k
 // 436; the 4096^2 -c -a matrix, one stream, 6.25 / 2.97 s; hd01 -c -m alone 108 / 55 ms).
 // Estimated from a sample of 16 KB (below): the byte of every run start (diff model applied), a
 // 256-bin histogram per wave in LDS, the top 16 by repeated max.
-constexpr int32_t kModeTables = -0x7A0, kModeCache = -0x7A1;
+constexpr int32_t kModeTables = -0x7A0, kModeCache = -0x7A1, kModeSmall = -0x7A2;
+// small alphabet: at most this many distinct run-start bytes in the sample (grad -c -m: 2)
+constexpr uint32_t kSmallVote = 4;
 template <int kSrc>
 __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_occ, uint32_t forced)
 {
@@ -1278,7 +1284,7 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
     const uint32_t sid = blockIdx.x * 4 + wv;
     if (sid >= bt.n) return;
     if (forced) {
-        if (lane == 0) bt.status[sid] = forced == 2 ? kModeTables : kModeCache;
+        if (lane == 0) bt.status[sid] = forced == 2 ? kModeTables : (forced == 3 ? kModeSmall : kModeCache);
         return;
     }
     uint32_t *h = hist[wv];
@@ -1334,13 +1340,19 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
         }
     }
     const bool cache = total == 0 || 100ull * top >= 60ull * total || (100ull * top >= 9ull * total && !low_occ);
-    if (lane == 0) bt.status[sid] = cache ? kModeCache : kModeTables;
+    // the distinct run-start bytes: at most kSmallVote -> the small-alphabet launch (whose steps
+    // need <= 16 FGK symbols; a stream whose count bytes widen the alphabet falls back to the
+    // regular batches there)
+    uint32_t distinct = 0;
+    for (uint32_t k = 0; k < 4; ++k) distinct += (uint32_t)__builtin_popcountll(ballot(h[64 * k + lane] != 0));
+    const bool small = total != 0 && distinct <= kSmallVote;
+    if (lane == 0) bt.status[sid] = small ? kModeSmall : (cache ? kModeCache : kModeTables);
 }
 
-template <int kW, int kSrc, bool kTab = false>
+template <int kW, int kSrc, bool kTab = false, bool kSmall = false>
 __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW, kTab>))) void encode_kernel(Batch bt)
 {
-    __shared__ Tree<kW, false, kTab> trees[kWaves];
+    __shared__ Tree<kW, false, kTab, kSmall> trees[kWaves];
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
@@ -1358,11 +1370,15 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // other layouts' launches skip the stream
     const uint64_t max_sym = kSrc == SRC_SYMBOLS ? n : n + n / 3 + 2;
     if (tree_kind(max_sym, bt.min_tree) != (uint32_t)kW) return;
-    // narrow and wide: the cache and the table launches split the streams (enc_mode_kernel)
-    if (kW <= 1 && (uni(bt.status[sid]) == kModeTables) != kTab) return;
+    // narrow and wide: the cache, table and (narrow) small-alphabet launches split the streams
+    // (enc_mode_kernel; a wide stream voted small takes the cache launch)
+    if (kW <= 1) {
+        const int32_t mode = (int32_t)uni((uint32_t)bt.status[sid]);
+        if ((mode == kModeTables) != kTab || (kW == 0 && mode == kModeSmall) != kSmall) return;
+    }
     const uint32_t window = window_bytes();
 
-    Fgk<kW, false, kTab> fgk(trees[wv], lane);
+    Fgk<kW, false, kTab, kSmall> fgk(trees[wv], lane);
     RecSink sink;
     sink.rs = make_rsrc(bt.out + out_off, (uint32_t)min(cap, (uint64_t)kMaxBufBytes));
     sink.wbase = 0;
@@ -1488,9 +1504,13 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             }
             sink.n = rl;
             if (rl == 64) {
+#ifndef HC_PROF_PASS
                 HC_PROF_BEGIN();
                 sink.pack();
                 HC_PROF_END(3);
+#else
+                sink.pack();
+#endif
             }
         }
     };
@@ -1520,6 +1540,21 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // seven symbols in groups of nine lanes (levels 0..8: every cached path), the root's
     // increments by lane 63 in the same adds (measured: six symbols in groups of ten, the root in
     // each group, C5 encode 369 ms against 349)
+    // Small alphabets (narrow layout, while at most 16 symbols are seen, so every position is >=
+    // 480; model: tests/fgk_batch_model.py small_len, encode(small=True)). A run-heavy stream with a
+    // few symbols (grad -c -m: 1, 3, 250, 255) ties on every row, and the tentative test below
+    // counts no earlier batch symbol through the next position: it ends a batch every ~4 symbols
+    // (1034 batches and 523 symbols alone per 512x512 stream). Here the counts are exact and the
+    // paths short, so up to 15 symbols go per step, four lanes each (levels 0..3: depth <= 4;
+    // lane 63 holds the root): every path position ORs its symbol's bit into a membership mark
+    // (smark, 2 positions per word), and symbol j's test at position a reads the pre-batch words
+    // of a and a + 1 and the marks of both: with c0 / c1 the earlier symbols through a / a + 1
+    // (c1 = j at the root: every symbol passes it) the level passes iff weight(a + 1) + c1 >=
+    // weight(a) + c0 + 1 -- the one-symbol loop's leader test on the tree as the earlier symbols
+    // leave it. The first symbol with a failing level (or no cached path, or a path deeper than
+    // four) ends the step: the ones before it commit with one add, it is coded alone. grad:
+    // 319 steps and 13 symbols alone per stream. Returns where the regular batches take over.
+    constexpr uint32_t kSG = 4, kSK = 15, kSmallNyt = kRoot - 32;
     constexpr uint32_t kBatch = 7, kLv = 9;  // (the masks: groups9)
     static_assert(kBatch * kLv <= 63 && kLv >= kInsertDepth, "batch lanes: every cached path, lane 63 free");
     constexpr uint32_t kIncU = kW ? 1u : 1024u;
@@ -1533,108 +1568,187 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         const uint32_t scb = lds_off(fgk.scr32());
         const uint32_t svb = (uint32_t)(size_t)(const lds_u8 *)sb + bj;
         const uint32_t lkl = lane * kLv;
+        constexpr uint64_t kL63 = 1ull << 63;
         uint32_t t = 0;
-        while (t < ns) {
-            if (sink.n > 64 - kBatch) sink.pack();
-            HC_CNT(1);
-            const uint32_t jmax = min(kBatch, ns - t);
-            const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + t));
-            const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
-            const uint32_t e = wh >> 10;
-            uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
-            // lane 63 (idle) holds the root and adds one increment per batch symbol
-            constexpr uint64_t kL63 = 1ull << 63;
-            pos = sel(idle, kRoot, pos);
-            const uint32_t wa = wtb + 4 * pos;
-            const uint64_t am = (ballot(pos < kRoot) & groups9(jmax)) | (jmax ? kL63 : 0);
-            const uint32_t vinc = sel(kL63, jmax * kIncU, kIncU);
-            // 1. tentative increments (each path position once, the root once per symbol)
-            const uint32_t w1 = *(const lds_u32 *)(size_t)(wa + 4);
-            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am, wa, scb), vinc, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
-            const uint32_t wn = *(const lds_u32 *)(size_t)wa;
-            // 2. the tests; 3. the increments from the first failing symbol on taken back
-            const uint64_t missm = ballot(pos == kMissPos);
-            uint64_t fm = (ballot(w1 < wn) & am) | missm;
-            uint32_t jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
-            if (jf < jmax) {
-                const uint32_t vdec = sel(kL63, (jf - jmax) * kIncU, 0u - kIncU);
-                __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~groups9(jf), wa, scb),
-                                       vdec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#if HC_BATCH_RETRY
-                // 4. retest in place (tests/fgk_batch_model.py retry_len). The failure of symbol jf
-                // may be false: its test counted no earlier batch symbol through the next position
-                // a + 1 (c1 = 0) and every later one through its own a. With the symbols before it
-                // committed and the ones from it on taken back, the words of a and a + 1 hold the
-                // exact counts of the earlier symbols, so the same tentative test run again on
-                // symbols jf.. is exact for jf unless a later symbol passes a, and stays
-                // conservative for the rest. Run when the failure can be false -- the first
-                // failing lane is no miss, jf > 0, and an earlier symbol holds a + 1 or a later
-                // one a (register compares) -- and again while it moves jf on. grad -c -m: the
-                // four-symbol alphabet's ties end a batch every ~4 symbols on c1 alone
-                // (slot-form model: 1034 batches + 523 symbols alone per stream -> 671 + 15).
-                uint32_t j0 = 0;
-                while (jf > j0) {
-                    const uint32_t fl = ff1(fm);
-                    if ((missm >> fl) & 1u) {
-                        HC_CNT(5);
-                        break;
-                    }
-                    const uint64_t gl = groups9(jf);
-#if HC_BATCH_RETRY == 1
-                    const uint32_t fa = lane_read(pos, fl);
-                    if (!((ballot(pos == fa + 1) & gl) | (ballot(pos == fa) & am & ~groups9(jf + 1)))) {
-                        HC_CNT(4);
-                        break;
-                    }
-#endif
-                    HC_CNT(3);
-                    const uint64_t am2 = am & ~gl;  // symbols jf.. and the root lane
-                    const uint32_t w1r = *(const lds_u32 *)(size_t)(wa + 4);
-                    __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am2, wa, scb),
-                                           sel(kL63, (jmax - jf) * kIncU, kIncU), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    const uint32_t wnr = *(const lds_u32 *)(size_t)wa;
-                    fm = (ballot(w1r < wnr) & am2) | missm;
-                    j0 = jf;
-                    jf = min(ff1(fm) / kLv, jmax);
-                    if (jf > j0) HC_CNT(6);
-                    if (jf == jmax) break;
+        // small-alphabet steps (above) while the stream has seen <= 16 symbols; re-checked only
+        // after a symbol coded alone (splits happen there), so a regular step pays nothing for it
+        if constexpr (!kSmall) {
+            // (the path-cache kernel: one regular batch step per pass of this loop)
+            while (t < ns) {
+                uint32_t jf, jmax;
+                if (sink.n > 64 - kBatch) sink.pack();
+                HC_CNT(1);
+                jmax = min(kBatch, ns - t);
+                const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + t));
+                const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
+                const uint32_t e = wh >> 10;
+                uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
+                // lane 63 (idle) holds the root and adds one increment per batch symbol
+                pos = sel(idle, kRoot, pos);
+                const uint32_t wa = wtb + 4 * pos;
+                const uint64_t am = (ballot(pos < kRoot) & groups9(jmax)) | (jmax ? kL63 : 0);
+                const uint32_t vinc = sel(kL63, jmax * kIncU, kIncU);
+                // 1. tentative increments (each path position once, the root once per symbol)
+                const uint32_t w1 = *(const lds_u32 *)(size_t)(wa + 4);
+                __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am, wa, scb), vinc, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WAVEFRONT);
+                const uint32_t wn = *(const lds_u32 *)(size_t)wa;
+                // 2. the tests; 3. the increments from the first failing symbol on taken back
+                const uint64_t fm = (ballot(w1 < wn) & am) | ballot(pos == kMissPos);
+                jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
+                if (jf < jmax) {
+                    const uint32_t vdec = sel(kL63, (jf - jmax) * kIncU, 0u - kIncU);
                     __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~groups9(jf), wa, scb),
-                                           sel(kL63, (jf - jmax) * kIncU, 0u - kIncU), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+                                           vdec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                 }
-#endif
+                const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
+                // the code record 1 << d | bits (bit k: level k's parity, left = even) from two
+                // ballots: the group's parity bits below its first root lane
+                const uint64_t par = ballot(pos & 1u), rtm = ballot(pos == kRoot);
+                const uint32_t gb = lkl - sink.n * kLv;  // q * kLv
+                const uint32_t d = (uint32_t)__builtin_ctz((uint32_t)(rtm >> gb) | (1u << kLv));
+                const uint32_t r = __builtin_amdgcn_ubfe((uint32_t)(par >> gb), 0, d) | (1u << d);
+                sink.vrec = q < jf ? r : sink.vrec;
+                __builtin_amdgcn_wave_barrier();
+                sink.n += jf;
+                t += jf;
+                if (jf < jmax) {  // symbol t: not cached, or a level reported (small: deeper than 4): alone
+                    HC_CNT(2);
+                    if (sink.n == 64) sink.pack();
+                    const uint32_t sym = uni(sb[t]);
+                    const uint32_t ent = uni(fgk.T.where[sym]) >> 10;
+                    if (ent == 0) {
+                        HC_PROF_BEGIN();
+                        miss(sym);
+                        HC_PROF_END(1);
+                    } else {
+                        HC_PROF_BEGIN();
+                        uint32_t pv;
+                        const uint32_t rc = fgk.pc_use(ent, fgk.pc_lane[ent * kRow], pv);
+                        sink.push(rc);
+                        fgk.update_path(pv);
+                        HC_PROF_END(2);
+                    }
+                    ++t;
+                }
             }
-            const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
-            // the code record 1 << d | bits (bit k: level k's parity, left = even) from two ballots:
-            // the group's parity bits below its first root lane
-            const uint64_t par = ballot(pos & 1u), rtm = ballot(pos == kRoot);
-            const uint32_t gb = lkl - sink.n * kLv;  // q * kLv
-            const uint32_t d = (uint32_t)__builtin_ctz((uint32_t)(rtm >> gb) | (1u << kLv));
-            const uint32_t r = __builtin_amdgcn_ubfe((uint32_t)(par >> gb), 0, d) | (1u << d);
-            sink.vrec = q < jf ? r : sink.vrec;
-            __builtin_amdgcn_wave_barrier();
-            sink.n += jf;
-            t += jf;
-            if (jf < jmax) {  // symbol t: not cached, or a level reported: coded alone
-                HC_CNT(2);
-                if (sink.n == 64) sink.pack();
-                const uint32_t sym = uni(sb[t]);
-                const uint32_t ent = uni(fgk.T.where[sym]) >> 10;
-                if (ent == 0) {
-                    HC_PROF_BEGIN();
-                    miss(sym);
-                    HC_PROF_END(1);
+        } else {
+            bool small = fgk.nyt >= kSmallNyt;
+            while (t < ns) {
+                uint32_t jf, jmax;
+                if (small) {
+                    // (the lane index opaque: these per-lane values are made here, not hoisted to the
+                    // kernel's entry beside the regular step's)
+                    const uint32_t ln = vreg(lane);
+                    const uint32_t g = ln < kSK * kSG ? ln >> 2 : kSK;  // the lane's symbol (kSK: idle)
+                    const uint32_t srow = lds_off16(&fgk.T.pc[0]) + 2 * (ln & 3u) - 2 * kRow;
+                    const uint32_t ssv = (uint32_t)(size_t)(const lds_u8 *)sb + (g < kSK ? g : 0u);
+                    const uint32_t sscb = lds_off(&fgk.T.scratch[0]) + 4 * ln;
+                    const uint32_t mkb = lds_off(&fgk.T.smark[0]);
+                    do {
+                        if (sink.n > 64 - kSK) sink.pack();
+                        HC_CNT(1);
+                        jmax = min(kSK, ns - t);
+                        const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(ssv + t));
+                        const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
+                        const uint32_t ra = srow + 32 * (wh >> 10);
+                        uint32_t pos = opaque(*(const lds_u16 *)(size_t)ra);
+                        const uint32_t p4 = opaque(*(const lds_u16 *)(size_t)(ra + 8));  // lane l = 0: level 4
+                        pos = sel(~0ull << (kSK * kSG), kRoot, pos);
+                        const uint32_t wa = wtb + 4 * pos;
+                        const uint64_t gm = below_mask(kSG * jmax);
+                        const uint64_t am = ballot(pos < kRoot) & gm;
+                        // no cached path, or one deeper than four: the step ends there
+                        const uint64_t em = (ballot(pos == kMissPos) | ballot((ln & 3u) == 0 && p4 != kRoot)) & gm;
+                        const uint32_t w0 = *(const lds_u32 *)(size_t)wa, w1 = *(const lds_u32 *)(size_t)(wa + 4);
+                        const uint32_t ma = pos - kSmallNyt, odd = ma & 1u;  // (pos >= 480 on the am lanes)
+                        const uint32_t mda = sel(am, mkb + 4 * (ma >> 1), sscb);
+                        __hip_atomic_fetch_or((uint32_t *)(lds_u32 *)(size_t)mda, (1u << g) << (odd << 4),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        // the marks of a (half `odd` of its word) and a + 1 (the other half, or the next word)
+                        const uint32_t mlo = *(const lds_u32 *)(size_t)mda;
+                        const uint32_t mhi = *(const lds_u32 *)(size_t)(mda + 4 * odd);
+                        const uint32_t c0 = (uint32_t)__builtin_popcount(__builtin_amdgcn_ubfe(mlo, odd << 4, g));
+                        const uint32_t c1 = pos + 1 == kRoot ? g
+                                                             : (uint32_t)__builtin_popcount(__builtin_amdgcn_ubfe(odd ? mhi : mlo, (odd ^ 1u) << 4, g));
+                        const uint64_t fm = (ballot((w1 >> 10) + c1 < (w0 >> 10) + c0 + 1) & am) | em;
+                        jf = min(ff1(fm) >> 2, jmax);
+                        // symbols < jf commit (+1 per path position and symbol, the root once each: lane
+                        // 63); the marks are cleared
+                        __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel((am & below_mask(kSG * jf)) | kL63, wa, sscb),
+                                               sel(kL63, jf << 10, 1u << 10), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        *(lds_u32 *)(size_t)mda = 0u;
+                        // code records (as below): record lane sink.n + q takes symbol q's
+                        const uint32_t q = ln - sink.n;
+                        const uint64_t par = ballot(pos & 1u), rtm = ballot(pos == kRoot);
+                        const uint32_t gb = kSG * q;
+                        const uint32_t d = (uint32_t)__builtin_ctz((uint32_t)(rtm >> gb) | (1u << kSG));
+                        const uint32_t r = __builtin_amdgcn_ubfe((uint32_t)(par >> gb), 0, d) | (1u << d);
+                        sink.vrec = q < jf ? r : sink.vrec;
+                        __builtin_amdgcn_wave_barrier();
+                        sink.n += jf;
+                        t += jf;
+                    } while (jf == jmax && t < ns);
                 } else {
-                    HC_PROF_BEGIN();
-                    uint32_t pv;
-                    const uint32_t rc = fgk.pc_use(ent, fgk.pc_lane[ent * kRow], pv);
-                    sink.push(rc);
-                    fgk.update_path(pv);
-                    HC_PROF_END(2);
+                    do {
+                        if (sink.n > 64 - kBatch) sink.pack();
+                        HC_CNT(1);
+                        jmax = min(kBatch, ns - t);
+                        const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(svb + t));
+                        const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
+                        const uint32_t e = wh >> 10;
+                        uint32_t pos = opaque(*(const lds_u16 *)(size_t)(rowb + 32 * e));
+                        // lane 63 (idle) holds the root and adds one increment per batch symbol
+                        pos = sel(idle, kRoot, pos);
+                        const uint32_t wa = wtb + 4 * pos;
+                        const uint64_t am = (ballot(pos < kRoot) & groups9(jmax)) | (jmax ? kL63 : 0);
+                        const uint32_t vinc = sel(kL63, jmax * kIncU, kIncU);
+                        // 1. tentative increments (each path position once, the root once per symbol)
+                        const uint32_t w1 = *(const lds_u32 *)(size_t)(wa + 4);
+                        __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am, wa, scb), vinc, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        const uint32_t wn = *(const lds_u32 *)(size_t)wa;
+                        // 2. the tests; 3. the increments from the first failing symbol on taken back
+                        const uint64_t fm = (ballot(w1 < wn) & am) | ballot(pos == kMissPos);
+                        jf = min(ff1(fm) / kLv, jmax);  // the failing lane's symbol
+                        if (jf < jmax) {
+                            const uint32_t vdec = sel(kL63, (jf - jmax) * kIncU, 0u - kIncU);
+                            __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel(am & ~groups9(jf), wa, scb),
+                                                   vdec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        }
+                        const uint32_t q = lane - sink.n;  // record lane q of the batch: symbol q's record
+                        // the code record 1 << d | bits (bit k: level k's parity, left = even) from two
+                        // ballots: the group's parity bits below its first root lane
+                        const uint64_t par = ballot(pos & 1u), rtm = ballot(pos == kRoot);
+                        const uint32_t gb = lkl - sink.n * kLv;  // q * kLv
+                        const uint32_t d = (uint32_t)__builtin_ctz((uint32_t)(rtm >> gb) | (1u << kLv));
+                        const uint32_t r = __builtin_amdgcn_ubfe((uint32_t)(par >> gb), 0, d) | (1u << d);
+                        sink.vrec = q < jf ? r : sink.vrec;
+                        __builtin_amdgcn_wave_barrier();
+                        sink.n += jf;
+                        t += jf;
+                    } while (jf == jmax && t < ns);
                 }
-                ++t;
+                if (jf < jmax) {  // symbol t: not cached, or a level reported (small: deeper than 4): alone
+                    HC_CNT(2);
+                    if (sink.n == 64) sink.pack();
+                    const uint32_t sym = uni(sb[t]);
+                    const uint32_t ent = uni(fgk.T.where[sym]) >> 10;
+                    if (ent == 0) {
+                        HC_PROF_BEGIN();
+                        miss(sym);
+                        HC_PROF_END(1);
+                    } else {
+                        HC_PROF_BEGIN();
+                        uint32_t pv;
+                        const uint32_t rc = fgk.pc_use(ent, fgk.pc_lane[ent * kRow], pv);
+                        sink.push(rc);
+                        fgk.update_path(pv);
+                        HC_PROF_END(2);
+                    }
+                    ++t;
+                    small = kSmall && fgk.nyt >= kSmallNyt;
+                }
             }
         }
     };
@@ -1773,9 +1887,13 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             }
             sink.n = rl;
             if (rl == 64) {
+#ifndef HC_PROF_PASS
                 HC_PROF_BEGIN();
                 sink.pack();
                 HC_PROF_END(3);
+#else
+                sink.pack();
+#endif
             }
         }
     };
@@ -1883,7 +2001,15 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
             }
             if (full || (!more && np)) {  // the serial FGK pass over the pending symbols
                 if constexpr (kTab) code_all_tab(np);
-                else if constexpr (kW <= 1 && HC_ENC_BATCH) code_all_batch(np);
+                else if constexpr (kW <= 1 && HC_ENC_BATCH) {
+#ifdef HC_PROF_PASS  // (diagnostic: region 3 times the whole batch pass instead of the record packing)
+                    HC_PROF_BEGIN();
+                    code_all_batch(np);
+                    HC_PROF_END(3);
+#else
+                    code_all_batch(np);
+#endif
+                }
                 else code_all(np);
                 nsym += np;
                 np = 0;
@@ -2616,6 +2742,12 @@ static hipError_t launch_encode_src(const Batch &b, dim3 grid, dim3 block, hipSt
             if (e == hipSuccess) e = e2;
         }
     }
+    // the small-alphabet streams last, after the join: its batch (grad: 8192 streams, one round of
+    // waves) must not share the CUs with the other launches' workgroups while they start and exit
+    // (launched first, beside the table launches: grad encode 1.23 -> 2.52 ms; after the cache
+    // launches but before the join: 1.6 ms)
+    encode_kernel<0, kSrc, false, true><<<grid, block, 0, st>>>(b);
+    if (e == hipSuccess) e = hipGetLastError();
     if (fork) (void)hipEventDestroy(fork);  // (released once the recorded work completes)
     if (join) (void)hipEventDestroy(join);
     return e;
@@ -2674,8 +2806,9 @@ extern "C" int hc_debug_set_min_tree(uint32_t kind)
 
 extern "C" int hc_debug_set_enc_tab(uint32_t mode)
 {
-    // 0: per stream (sampled alphabet), 1: path cache for every stream, 2: tables for every stream
-    hc::g_enc_tab = mode > 2 ? 0 : mode;
+    // 0: per stream (sampled alphabet), 1: path cache for every stream, 2: tables for every
+    // stream, 3: the small-alphabet kernel for every stream (narrow layout)
+    hc::g_enc_tab = mode > 3 ? 0 : mode;
     return 0;
 }
 

@@ -75,7 +75,29 @@ def retry_len(t, paths):
         j0 = jf
 
 
-def encode(symbols, batched, misses=False, lanes=9, exact=False, retry=False):
+SMALL_NYT = ROOT - 32  # small-alphabet batches while at most 16 symbols are seen (positions >= 480)
+SMALL_G, SMALL_K = 4, 15  # ... with four lanes per symbol (depth <= 4) and fifteen symbols per step
+
+
+def small_len(t, paths):
+    """the encoder's small-alphabet batch (hc_fgk.hip code_small): exact counts -- symbol j's test
+    at position a counts the earlier batch symbols through a (c0) and through a + 1 (c1; every
+    earlier one when a + 1 is the root) from membership marks -- so jf = the first symbol whose
+    update would swap (or end at the NYT's parent), exactly as the one-symbol loop finds it"""
+    for j, p in enumerate(paths):
+        if p is None:
+            return j
+        for a in p:
+            if a == ROOT:
+                break
+            c0 = sum(1 for q in paths[:j] if a in q)
+            c1 = j if a + 1 == ROOT else sum(1 for q in paths[:j] if (a + 1) in q)
+            if t.w[a + 1] + c1 < t.w[a] + c0 + 1:
+                return j
+    return len(paths)
+
+
+def encode(symbols, batched, misses=False, lanes=9, exact=False, retry=False, small=False):
     """(codes, tree, stats): every symbol's code bits and the final tree; batched=False is the
     one-symbol loop, True the batched one (the kernel's tentative test; exact=True: exact counts).
     misses=True (measured and dropped): a symbol that has a leaf but no cached path joins the batch
@@ -104,7 +126,7 @@ def encode(symbols, batched, misses=False, lanes=9, exact=False, retry=False):
         for s, lead in t.swaps:
             pc.on_swap(s, lead)
 
-    def cached(sym):
+    def cached(sym, depth=99):
         e = pc.slot.get(sym)
         if t.where[sym] == 0:
             return None
@@ -113,13 +135,31 @@ def encode(symbols, batched, misses=False, lanes=9, exact=False, retry=False):
                 return None
             p = t.path(t.where[sym]) + [ROOT]
             return p if len(p) <= lanes else None
-        return pc.ent[e][1] + [ROOT]
+        return pc.ent[e][1] + [ROOT] if len(pc.ent[e][1]) <= depth else None
 
     i, n = 0, len(symbols)
     while i < n:
         if not batched:
             alone(symbols[i])
             i += 1
+            continue
+        if small and t.nyt >= SMALL_NYT:  # exact batches of up to SMALL_K symbols of depth <= SMALL_G
+            paths = []
+            for s_ in symbols[i:i + SMALL_K]:
+                paths.append(cached(s_, SMALL_G))
+                if paths[-1] is None:
+                    break
+            jf = small_len(t, paths)  # (more exact than batch_len, which never counts the root as c1)
+            stats["small"] = stats.get("small", 0) + 1
+            for p in paths[:jf]:
+                codes.append([a & 1 for a in reversed(p[:-1])])
+                for a in p:
+                    t.w[a] += 1
+            i += jf
+            if jf < len(paths):
+                stats["alone"] += 1
+                alone(symbols[i])
+                i += 1
             continue
         paths = [cached(s) for s in symbols[i:i + BATCH]]
         jf = batch_len(t, paths) if exact else (retry_len if retry else tentative_len)(t, paths)

@@ -2,8 +2,9 @@
 
 Cache mode keeps the root paths of recently coded symbols (hc_fgk.hip Fgk::pc_*); table mode
 keeps the decoder's level tables plus each position's code (pcode[]) and checks every lookup
-against the tables (hc_fgk.hip code_all_tab). hc_debug_set_enc_tab forces either mode for every stream, and both must
-produce the reference's bytes: its digests, edge vectors, deep / skewed trees (vs the oracle)
+against the tables (hc_fgk.hip code_all_tab); the small-alphabet kernel is cache mode with exact
+15-symbol steps while a stream has seen <= 16 symbols (tests/test_gpu_small.py).
+hc_debug_set_enc_tab forces one mode for every stream, and each must produce the reference's bytes: its digests, edge vectors, deep / skewed trees (vs the oracle)
 and the adaptive symbol streams; by default (mode 0) enc_mode_kernel picks per stream. Reference: huffman.cpp:136-155 (code of a symbol),
 huffman.cpp:95-128 (update), transform.cpp:363-384 (applyHuffman).
 """
@@ -21,7 +22,7 @@ def sha(b):
     return hashlib.sha256(b).hexdigest()
 
 
-@pytest.fixture(params=[2, 1, 0], ids=["tables", "cache", "auto"])
+@pytest.fixture(params=[2, 1, 3, 0], ids=["tables", "cache", "small", "auto"])
 def enc_mode(request, gpu, hc):
     hc.use_debug_build(True)  # the hook exists in the debug build only
     hc.debug_set_enc_tab(request.param)
