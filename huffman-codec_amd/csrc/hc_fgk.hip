@@ -52,15 +52,20 @@ static uint32_t g_min_tree = 0;
 // encoder mode for narrow / wide streams: 0 = per stream by enc_mode_kernel (default), 1 = path
 // cache for all, 2 = tables for all (hc_debug_set_enc_tab; tests run both on every input)
 static uint32_t g_enc_tab = 0;
+// decoder launch for narrow streams: 0 = by payload rate (dec_small_stream), 1 = small-alphabet
+// for all, 2 = regular for all (hc_debug_set_dec_small)
+static uint32_t g_dec_small = 0;
 __device__ __forceinline__ uint64_t *trace_buf() { return g_trace; }
 __device__ __forceinline__ uint32_t window_bytes() { return __builtin_amdgcn_readfirstlane(g_window); }
 static uint32_t min_tree() { return g_min_tree; }
 static uint32_t enc_tab() { return g_enc_tab; }
+static uint32_t dec_small() { return g_dec_small; }
 #else
 __device__ __forceinline__ uint64_t *trace_buf() { return nullptr; }
 __device__ __forceinline__ uint32_t window_bytes() { return 1u << 30; }
 static uint32_t min_tree() { return 0; }
 static uint32_t enc_tab() { return 0; }
+static uint32_t dec_small() { return 0; }
 #endif
 // Streams are addressed through buffer descriptors, whose offsets are 32-bit: each stream's input
 // and output are reached through windows that slide forward by whole multiples of 256 bytes
@@ -448,9 +453,9 @@ struct Fgk {
             T.body[i] = i == kRoot ? (kDec ? kNyt | kNotLeaf : kNyt) : 0;
             if (kWide) T.up[i] = 0;
         }
+        if (kSmall && lane < sizeof(T.smark) / 4) T.smark[lane] = 0;
         if (!kDec) {
             for (uint32_t i = lane; i < 256; i += 64) T.where[i] = 0;
-            if (kSmall && lane < sizeof(T.smark) / 4) T.smark[lane] = 0;
             if constexpr (kTab) {
                 for (uint32_t i = lane; i < 516; i += 64) T.pcode[i] = 0;
             } else {
@@ -1276,6 +1281,10 @@ constexpr int kWavesPerSimd = kTab ? (kW == 0 ? 6 : 5) : (kW == 0 ? HC_WPE0 : (k
 constexpr int32_t kModeTables = -0x7A0, kModeCache = -0x7A1, kModeSmall = -0x7A2;
 // small alphabet: at most this many distinct run-start bytes in the sample (grad -c -m: 2)
 constexpr uint32_t kSmallVote = 4;
+// the small-alphabet steps (encoder code_all_batch, decoder Dec::decode_small): kSmallK symbols
+// of kSmallG lanes (levels, depth <= kSmallG) each, while every position is >= kSmallNyt (at
+// most 16 symbols seen)
+constexpr uint32_t kSmallG = 4, kSmallK = 15, kSmallNyt = kRoot - 32;
 template <int kSrc>
 __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_occ, uint32_t forced)
 {
@@ -1554,7 +1563,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
     // leave it. The first symbol with a failing level (or no cached path, or a path deeper than
     // four) ends the step: the ones before it commit with one add, it is coded alone. grad:
     // 319 steps and 13 symbols alone per stream. Returns where the regular batches take over.
-    constexpr uint32_t kSG = 4, kSK = 15, kSmallNyt = kRoot - 32;
+    constexpr uint32_t kSG = kSmallG, kSK = kSmallK;
     constexpr uint32_t kBatch = 7, kLv = 9;  // (the masks: groups9)
     static_assert(kBatch * kLv <= 63 && kLv >= kInsertDepth, "batch lanes: every cached path, lane 63 free");
     constexpr uint32_t kIncU = kW ? 1u : 1024u;
@@ -2186,11 +2195,22 @@ __device__ __forceinline__ uint32_t revert_block(uint32_t x4, uint32_t m, RevCar
 // One stream's decoder (huffman.cpp:60-93 + transform.cpp:386-406 per symbol, then the RLE and
 // diff revert of transform.cpp:137-159 / 231-239 per 256-symbol block; header main.cpp:90-104).
 // decode_kernel runs one per wavefront.
-template <int kW, int kDst>
+// The small-alphabet launch (decode_kernel<0, .., true>, Dec::decode_small) takes the narrow
+// streams whose payload averages under 2.5 bits per symbol -- the header's count and the
+// stream's length, so the decoder needs no sample of its own (grad -c -m: 1.7; photo -c -m:
+// 3.3-3.6; noise, -c photos: ~8). mode (hc_debug_set_dec_small): 0 by the rate, 1 every narrow
+// stream, 2 none. Either launch decodes any stream exactly; the rate only picks the faster.
+__device__ __forceinline__ bool dec_small_stream(uint64_t count, uint64_t bits, uint32_t mode)
+{
+    if (mode) return mode == 1;
+    return count != 0 && bits * 2 < count * 5;
+}
+
+template <int kW, int kDst, bool kSmall = false>
 struct Dec {
     // symbol indices: 32-bit below 2^32 symbols (narrow / wide), 64-bit for the huge layout
     using Idx = std::conditional_t<kW == 2, uint64_t, uint32_t>;
-    Fgk<kW, true> fgk;
+    Fgk<kW, true, false, kSmall> fgk;
     BitSource in;
     uint32_t lane, sid, st, dmask;
     uint64_t len, cap, payload_bits;
@@ -2205,7 +2225,7 @@ struct Dec {
     bool batch_on = true;          // the next block runs batches
     uint64_t pacc = 0;  // HC_PROF regions
 
-    __device__ __forceinline__ Dec(Tree<kW, true> &t, uint32_t l) : fgk(t, l), lane(l) {}
+    __device__ __forceinline__ Dec(Tree<kW, true, false, kSmall> &t, uint32_t l) : fgk(t, l), lane(l) {}
 
     // the stream's header; false: nothing to decode here (its error status is written, or another
     // tree layout's launch owns it)
@@ -2233,8 +2253,11 @@ struct Dec {
             else if (kDst == DST_RAW && (flags & 0x40u)) st = HC_ERR_UNSUPPORTED;
         }
         if (st == 0 && tree_kind(count, bt.min_tree) != (uint32_t)kW) return false;  // another layout's launch owns it
+        // narrow streams under 2.5 payload bits per symbol go to the small-alphabet launch
+        // (dec_small_stream), the rest to the regular one
+        if (st == 0 && kW == 0 && dec_small_stream(count, (len - 9) * 8, bt.dec_small) != kSmall) return false;
         if (st != 0) {
-            if (kW == 0 && lane == 0) {
+            if (kW == 0 && !kSmall && lane == 0) {
                 bt.status[sid] = (int32_t)st;
                 bt.out_lens[sid] = 0;
             }
@@ -2527,6 +2550,85 @@ struct Dec {
         ++btry;
         return jf == jmax;
     }
+
+    // Small alphabets (the small-alphabet launch, narrow layout, while at most 16 symbols are
+    // seen: every position >= kSmallNyt; the encoder's small steps in code_all_batch, whose
+    // output this reads back). Up to 15 symbols of depth <= 4 per step, four lanes each (lane
+    // 4 j + l: level 4 - l of symbol j's lookup in the level tables); the chain of symbol starts
+    // from the level-4 depths at every bit offset (<= 4 bits a symbol: 60 bits at most). The
+    // leader tests are exact, as in the encoder: every path position ORs its symbol's bit into a
+    // membership mark (smark), and symbol j's test at position a reads the pre-step words of a
+    // and a + 1 and the marks of both: with c0 / c1 the earlier symbols through a / a + 1 (c1 = j
+    // at the root) the level passes iff weight(a + 1) + c1 >= weight(a) + c0 + 1. The first
+    // symbol with a failing level, or whose level-4 entry is no leaf (deeper than 4, or the
+    // NYT), ends the step: the ones before it commit with one add (the root by lane 63), it goes
+    // to the one-symbol step. Returns whether the step took every symbol the window and the
+    // block allowed.
+    __device__ __forceinline__ bool decode_small(Idx i0, Idx &i, Idx i1)
+    {
+        static_assert(kW == 0 && kSmall, "the small-alphabet launch: narrow layout");
+        constexpr uint32_t kSG = kSmallG, kSK = kSmallK;
+        constexpr uint64_t kL63 = 1ull << 63;
+        // (the lane index opaque: these per-lane values are made here, not hoisted beside the
+        // regular batch's)
+        const uint32_t ln = vreg(lane);
+        const uint32_t g = ln < kSK * kSG ? ln >> 2 : kSK;  // the lane's symbol (kSK: idle)
+        const uint32_t bl = ln & 3u;                        // its level: 4 - bl
+        const uint32_t bvb = lds_off16(&fgk.T.lvl[0]) + 2 * ((16u >> bl) - 2);
+        const uint32_t l4 = lds_off16(&fgk.T.lvl[14]);  // level 4
+        const uint32_t sscb = lds_off(&fgk.T.scratch[0]) + 4 * ln;
+        const uint32_t mkb = lds_off(&fgk.T.smark[0]);
+        const uint64_t w0 = in.win;
+        const uint32_t n0 = in.nwin;  // >= 33: symbols 0..7 always fit
+        // lane o: the depth of a code that starts o bits into the window (4 when deeper)
+        const uint32_t dep = opaque(*(const lds_u16 *)(size_t)(l4 + 2 * (uint32_t)((w0 << ln) >> 60))) >> 10;
+        uint32_t S = 0, sv = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kSK; ++j) {
+            sv = writelane(sv, S, j);
+            S += lane_read(dep, S);
+        }
+        sv = writelane(sv, S, kSK);
+        const uint32_t sg = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(g * 4), (int)sv);
+        const uint32_t nval = __builtin_popcountll(ballot(sv <= n0) & (((1ull << kSK) - 1) << 1));
+        const uint32_t jmax = min(nval, (uint32_t)(i1 - i));
+        const uint32_t ent = opaque(*(const lds_u16 *)(size_t)(bvb + (((uint32_t)((w0 << sg) >> 32) >> (28 + bl)) << 1)));
+        uint32_t pos = ent & 1023u;
+        pos = sel(~0ull << (kSK * kSG), kRoot, pos);  // lane 63: the root
+        const uint64_t gm = below_mask(kSG * jmax);
+        // each path position once (the entry stops at the lane's own level)
+        const uint64_t am = ballot((ent >> 10) == 4 - bl) & gm;
+        const uint32_t wa = lds_off(&fgk.T.wt[0]) + 4 * pos;
+        const uint32_t b = opaque(*(const lds_u16 *)(size_t)(lds_off16(&fgk.T.body[0]) + 2 * pos));
+        constexpr uint64_t kLeafLanes = 0x0111111111111111ull;  // level 4: lanes 4 j
+        const uint32_t jn = ff1(ballot(b & kNotLeaf) & kLeafLanes) >> 2;
+        const uint32_t wl = *(const lds_u32 *)(size_t)wa, wh = *(const lds_u32 *)(size_t)(wa + 4);
+        const uint32_t ma = pos - kSmallNyt, odd = ma & 1u;  // (pos >= 480 on the am lanes)
+        const uint32_t mda = sel(am, mkb + 4 * (ma >> 1), sscb);
+        __hip_atomic_fetch_or((uint32_t *)(lds_u32 *)(size_t)mda, (1u << g) << (odd << 4), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t mlo = *(const lds_u32 *)(size_t)mda;
+        const uint32_t mhi = *(const lds_u32 *)(size_t)(mda + 4 * odd);
+        const uint32_t c0 = (uint32_t)__builtin_popcount(__builtin_amdgcn_ubfe(mlo, odd << 4, g));
+        const uint32_t c1 = pos + 1 == kRoot ? g : (uint32_t)__builtin_popcount(__builtin_amdgcn_ubfe(odd ? mhi : mlo, (odd ^ 1u) << 4, g));
+        const uint64_t fm = ballot((wh >> 10) + c1 < (wl >> 10) + c0 + 1) & am;
+        const uint32_t jf = min(min(ff1(fm) >> 2, jn), jmax);
+        __hip_atomic_fetch_add((uint32_t *)(lds_u32 *)(size_t)sel((am & below_mask(kSG * jf)) | kL63, wa, sscb),
+                               sel(kL63, jf << 10, 1u << 10), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        *(lds_u32 *)(size_t)mda = 0u;
+        const uint32_t sb0 = (uint32_t)(size_t)(lds_u8 *)sbuf + (uint32_t)(i - i0);
+        *(lds_u8 *)(size_t)sel(kLeafLanes & below_mask(kSG * jf), sb0 + g, sscb) = (uint8_t)b;
+        __builtin_amdgcn_wave_barrier();
+        HC_CNT(1);
+        if (jf < jmax) HC_CNT(2);
+        const uint32_t sj = lane_read(sv, jf);
+        in.win = w0 << sj;
+        in.nwin = n0 - sj;
+        i += jf;
+        bsym += jf;
+        ++btry;
+        return jf == jmax;
+    }
 #endif
 
     // symbols i .. i1 - 1 of the block at i0, one stream
@@ -2550,7 +2652,9 @@ struct Dec {
             constexpr bool kOne = kBat && kW <= 1;
             if constexpr (kOne) {
                 HC_PROF_BEGIN();
-                const bool whole = decode_batch(i0, i, i1);
+                bool whole;
+                if constexpr (kSmall) whole = fgk.nyt >= kSmallNyt ? decode_small(i0, i, i1) : decode_batch(i0, i, i1);
+                else whole = decode_batch(i0, i, i1);
                 HC_PROF_END(6);
                 if (whole) continue;
                 if (in.nwin <= 32) in.refill();
@@ -2679,16 +2783,16 @@ struct Dec {
     }
 };
 
-template <int kW, int kDst>
+template <int kW, int kDst, bool kSmall = false>
 __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd<kW>))) void decode_kernel(Batch bt)
 {
-    __shared__ Tree<kW, true> trees[kWaves];
+    __shared__ Tree<kW, true, false, kSmall> trees[kWaves];
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t sid = blockIdx.x * kWaves + wv;
     if (sid >= bt.n) return;
-    Dec<kW, kDst> dec(trees[wv], lane);
+    Dec<kW, kDst, kSmall> dec(trees[wv], lane);
     if (!dec.open(bt, sid)) return;
     // two copies of the block loop, as in the encoder: without window bookkeeping for streams
     // that fit one window (input and output), with it for the rest
@@ -2773,15 +2877,20 @@ hipError_t launch_decode(const Batch &b0, DecDst dst, hipStream_t st)
     if (b0.n == 0) return hipSuccess;
     Batch b = b0;
     b.min_tree = min_tree();
+    b.dec_small = dec_small();
     const dim3 grid((b.n + kWaves - 1) / kWaves), block(64 * kWaves);
+    // one launch per tree layout, then the small-alphabet streams' (dec_small_stream), each
+    // stream decoded by exactly one of them
     if (dst == DST_RAW) {
         decode_kernel<0, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_RAW><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_RAW><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_RAW, true><<<grid, block, 0, st>>>(b);
     } else {
         decode_kernel<0, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<1, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
         decode_kernel<2, DST_SYMBOLS><<<grid, block, 0, st>>>(b);
+        decode_kernel<0, DST_SYMBOLS, true><<<grid, block, 0, st>>>(b);
     }
     return hipGetLastError();
 }
@@ -2801,6 +2910,13 @@ extern "C" int hc_debug_set_min_tree(uint32_t kind)
 {
     // 0 narrow, 1 wide, 2 huge: the smallest tree layout of every later FGK launch
     hc::g_min_tree = kind > 2 ? 2 : kind;
+    return 0;
+}
+
+extern "C" int hc_debug_set_dec_small(uint32_t mode)
+{
+    // 0: by payload rate, 1: the small-alphabet decoder for every narrow stream, 2: for none
+    hc::g_dec_small = mode > 2 ? 0 : mode;
     return 0;
 }
 

@@ -21,6 +21,7 @@ struct Batch {
     int32_t *status;
     uint32_t flags;  // header flags byte for SRC_SYMBOLS encodes
     uint32_t min_tree;  // set by the launchers: the smallest FGK tree layout (hc_debug_set_min_tree)
+    uint32_t dec_small;  // set by launch_decode: 0 by payload rate, 1 / 2 every / no narrow stream small (hc_debug_set_dec_small)
 };
 
 enum EncSrc { SRC_RAW = 0, SRC_RAW_DIFF = 1, SRC_SYMBOLS = 2 };

@@ -380,12 +380,24 @@ def debug_set_min_tree(kind):
 def debug_set_enc_tab(mode):
     """Test hook (debug build only, use_debug_build): how the encoder finds a symbol's code for
     narrow / wide streams: 0 per stream from a sample of its alphabet (the default), 1 the path
-    cache for every stream, 2 the level tables for every stream."""
+    cache for every stream, 2 the level tables for every stream, 3 the small-alphabet kernel for
+    every narrow stream."""
     f = _dbg().hc_debug_set_enc_tab
     f.argtypes = [ctypes.c_uint32]
     rc = f(int(mode))
     if rc:
         raise HCodecError(f"hc_debug_set_enc_tab failed: {rc}")
+
+
+def debug_set_dec_small(mode):
+    """Test hook (debug build only, use_debug_build): which decoder launch takes a narrow stream:
+    0 by its payload rate (under 2.5 bits per symbol: the small-alphabet launch; the default), 1
+    the small-alphabet launch for every one, 2 the regular launch for every one."""
+    f = _dbg().hc_debug_set_dec_small
+    f.argtypes = [ctypes.c_uint32]
+    rc = f(int(mode))
+    if rc:
+        raise HCodecError(f"hc_debug_set_dec_small failed: {rc}")
 
 
 def debug_enc_votes(inp, in_offs, in_lens, use_diff, low_occ, status, stream=None):

@@ -1,4 +1,4 @@
-"""GPU parity of the encoder's small-alphabet kernel (hc_fgk.hip encode_kernel<.., kSmall>, the
+"""GPU parity of the small-alphabet kernels -- the encoder's (hc_fgk.hip encode_kernel<.., kSmall>, the
 small steps of its code_all_batch; model: tests/fgk_batch_model.py small_len, checked against the
 one-symbol loop in tests/test_batch_model.py): while a stream has seen at most 16 symbols, up to
 15 cached symbols of depth <= 4 are coded per step with exact leader tests from membership marks.
@@ -8,7 +8,10 @@ whose alphabet grows past 16 partway (the steps hand over to the regular batches
 small-alphabet kernel forced on every stream, in the path-cache kernel, and through the automatic
 vote (enc_mode_kernel sends a stream whose sample has at most 4 distinct run-start bytes to the
 small kernel), with and without the diff model, byte for byte against the oracle
-(transform.cpp:363-384, huffman.cpp:95-217), then decoded back."""
+(transform.cpp:363-384, huffman.cpp:95-217), then decoded back -- by the decoder's small-alphabet
+launch (decode_kernel<0, .., true>, Dec::decode_small: the same steps read back from the level
+tables; chosen by payload rate under 2.5 bits per symbol, or forced for every narrow stream) and by
+the regular one."""
 import numpy as np
 import pytest
 
@@ -41,6 +44,22 @@ def _streams(oracle_mod):
     return raws
 
 
+def _decode_modes(hc, torch, encs, raws, modes=(0, 1, 2)):
+    """every stream decoded back by each decoder launch choice (hc_debug_set_dec_small: 0 by rate,
+    1 the small-alphabet launch for every narrow stream, 2 the regular launch for every one)"""
+    hc.use_debug_build(True)
+    try:
+        for dm in modes:
+            hc.debug_set_dec_small(dm)
+            st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
+            assert st == [0] * len(raws), dm
+            for i, (r, b) in enumerate(zip(raws, back)):
+                assert b == r, f"decoder mode {dm}, stream {i}"
+    finally:
+        hc.debug_set_dec_small(0)
+        hc.use_debug_build(False)
+
+
 @pytest.mark.parametrize("mode", [3, 1, 0], ids=["small", "cache", "vote"])
 @pytest.mark.parametrize("use_diff", [True, False], ids=["cm", "c"])
 def test_small_alphabet_steps_vs_oracle(gpu, hc, oracle_mod, use_diff, mode):
@@ -57,8 +76,66 @@ def test_small_alphabet_steps_vs_oracle(gpu, hc, oracle_mod, use_diff, mode):
     for i, (r, e) in enumerate(zip(raws, encs)):
         want = oracle_mod.compress(r, use_diff, False, 512)
         assert want[0] == 0 and e == want[1], f"stream {i} ({len(r)} bytes)"
+    # the shipping library's own choice, then each launch forced
     st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
-    assert st == [0] * len(raws) and back == raws
+    assert st == [0] * len(raws)
+    assert [i for i, (r, b) in enumerate(zip(raws, back)) if r != b] == []
+    if mode == 0:
+        _decode_modes(hc, torch, encs, raws)
+
+
+def test_small_alphabet_decoder_window_edges(gpu, hc, oracle_mod):
+    """decode_small's steps across the input window's edges and the 256-symbol block ends: the
+    grad / two-level streams under a 4 KB descriptor window, every narrow stream on the
+    small-alphabet launch"""
+    torch = gpu
+    raws = _streams(oracle_mod)[:12]
+    encs = [oracle_mod.compress(r, True, False, 512)[1] for r in raws]
+    hc.use_debug_build(True)
+    try:
+        hc.debug_set_window(4096)
+        for dm in (1, 2):
+            hc.debug_set_dec_small(dm)
+            st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
+            assert st == [0] * len(raws), dm
+            assert [i for i, (r, b) in enumerate(zip(raws, back)) if r != b] == [], dm
+    finally:
+        hc.debug_set_window(1 << 30)
+        hc.debug_set_dec_small(0)
+        hc.use_debug_build(False)
+
+
+def test_small_alphabet_decoder_damaged_streams(gpu, hc, oracle_mod):
+    """truncated and bit-flipped low-rate streams: the small-alphabet launch ends each with the
+    oracle's status (the regular launch's, transform.cpp:394-398) and never runs past its buffers"""
+    torch = gpu
+    raws = _streams(oracle_mod)[:8]
+    encs = [oracle_mod.compress(r, True, False, 512)[1] for r in raws]
+    bad = []
+    for k, e in enumerate(encs):
+        bad.append(e[: len(e) // 2])  # truncated: count says more symbols than the payload holds
+        b = bytearray(e)
+        b[9 + (k * 131) % (len(e) - 9)] ^= 0x5A  # a flipped payload byte
+        bad.append(bytes(b))
+    wants = [oracle_mod.decompress(blob) for blob in bad]
+    # capacity: the oracle's output exactly (a status-0 stream), or room to spare (an error
+    # status outranks the capacity check, HcStatus)
+    caps = [len(w[1]) if w[0] == 0 else 2 * len(raws[j // 2]) + 1024 for j, w in enumerate(wants)]
+    res = {}
+    hc.use_debug_build(True)
+    try:
+        for dm in (1, 2):
+            hc.debug_set_dec_small(dm)
+            res[dm] = decompress_batch(hc, torch, bad, caps)
+    finally:
+        hc.debug_set_dec_small(0)
+        hc.use_debug_build(False)
+    for j, want in enumerate(wants):
+        for dm in (1, 2):
+            st, back, _ = res[dm]
+            assert st[j] == want[0], (dm, j)
+            if want[0] == 0:
+                assert back[j] == want[1], (dm, j)
 
 
 def test_small_alphabet_grad_batch_digests(gpu, hc, oracle_mod):
@@ -79,6 +156,8 @@ def test_small_alphabet_grad_batch_digests(gpu, hc, oracle_mod):
     st, encs, _ = compress_batch(hc, torch, raws, True)
     assert st == [0] * len(raws)
     st, back, _ = decompress_batch(hc, torch, encs, [len(r) for r in raws])
-    assert st == [0] * len(raws) and back == raws
+    assert st == [0] * len(raws)
+    assert [i for i, (r, b) in enumerate(zip(raws, back)) if r != b] == []
+    _decode_modes(hc, torch, encs[:32], raws[:32], (1, 2))
     for k in (0, 77, 255):
         assert encs[k] == oracle_mod.compress(raws[k], True, False, 512)[1]
