@@ -1935,31 +1935,9 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
         constexpr uint32_t kQ = HC_SPARSE_KB, kBC = 4 * kQ;  // KB and 256-byte chunks per block
         bool sparse = false;
         u32x4 blk[kQ] = {};
-#ifndef HC_SPARSE_PRE2
-#define HC_SPARSE_PRE2 0
-#endif
-        // kPre2: two blocks in flight (the small-alphabet kernel: grad's blocks take less time
-        // than a load)
-        constexpr bool kPre2 = HC_SPARSE_PRE2 && kSmall;
-        u32x4 blk2[kPre2 ? kQ : 1] = {};
         auto load_blk = [&](uint32_t c0) __attribute__((always_inline)) {
-            if constexpr (kPre2) {
 #pragma unroll
-                for (uint32_t i = 0; i < kQ; ++i) {
-                    blk[i] = blk2[i];
-                    blk2[i] = buf_load4(rin, 256 * (c0 + kBC) + 16 * (kQ * lane + i));
-                }
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < kQ; ++i) blk[i] = buf_load4(rin, 256 * c0 + 16 * (kQ * lane + i));
-            }
-        };
-        auto enter_blk = [&](uint32_t c0) __attribute__((always_inline)) {
-#pragma unroll
-            for (uint32_t i = 0; i < kQ; ++i) {
-                blk[i] = buf_load4(rin, 256 * c0 + 16 * (kQ * lane + i));
-                if constexpr (kPre2) blk2[i] = buf_load4(rin, 256 * (c0 + kBC) + 16 * (kQ * lane + i));
-            }
+            for (uint32_t i = 0; i < kQ; ++i) blk[i] = buf_load4(rin, 256 * c0 + 16 * (kQ * lane + i));
         };
         for (uint32_t ci = 0;;) {
             const bool more = ci < nch && !fgk.bad;
@@ -2020,7 +1998,7 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                     HC_PROF_END(4);
                     if (kSparseOn && !full && slanes <= kSparseEnter && ci + 1 + kBC < nch) {
                         sparse = true;  // the block at ci + 1 (the chunk loaded ahead is dropped)
-                        enter_blk(ci + 1);
+                        load_blk(ci + 1);
                     }
                     if (kWin) {
                         full = !full;  // code this chunk's symbols now (the chunk itself always fits)
