@@ -303,12 +303,15 @@ def roofline(S, N, enc_bytes, enc_ms, dec_ms, mode, kind):
     if os.path.exists(PMC_PATH):
         with open(PMC_PATH) as f:
             pm = json.load(f)
-        key = f"{dom}:{mode}:{kind}:{S}"
-        e = pm.get("launches", {}).get(key)
-        et = pm.get("launches", {}).get(f"{dom}_tables:{mode}:{kind}:{S}")
-        if e and et:  # the encoder's two mode launches (path cache, level tables) run side by side
-            e = {k: e.get(k, 0) + et.get(k, 0) for k in ("hbm_bytes", "valu_salu_insts")}
-            key += " + " + f"{dom}_tables:{mode}:{kind}:{S}"
+        # each stream is coded by one launch of the kernel's family (path cache / level tables /
+        # small alphabet): the workload's counters are their sum
+        keys = [f"{dom}{v}:{mode}:{kind}:{S}" for v in ("", "_tables", "_small")]
+        parts = [pm.get("launches", {}).get(k) for k in keys]
+        key = " + ".join(k for k, p in zip(keys, parts) if p)
+        e = None
+        if key:
+            e = {c: sum(p.get(c, 0) for p in parts if p) for c in ("hbm_bytes", "valu_salu_insts")
+                 if all(c in p for p in parts if p)}
         if e and pm.get("source_sha") == src_sha():
             r["traffic"] = e.get("hbm_bytes")
             r["traffic_source"] = f"profiles/pmc_summary.json[{key}] (rocprofv3 PMC, same kernel source)"

@@ -32,15 +32,17 @@ FGK_SRC = os.path.join(ROOT, "huffman-codec_amd", "csrc", "hc_fgk.hip")
 def kernel_key(name):
     """encode_kernel<0, 1, false> (tree layout 0 = narrow, source 1, path-cache mode; round-1 builds:
     <false, 1>) -> ('encode_kernel', narrow, source / destination kind). The table-mode launch of
-    the same layout (<0, 1, true>) is keyed apart: on the -c -m headline its waves exit at once."""
+    the same layout (<0, 1, true>) and the small-alphabet launches (encode_kernel<0, 1, false, true>,
+    decode_kernel<0, 0, true>) are keyed apart (_tables, _small): each stream is coded by one
+    of them, so a workload's total is their sum."""
     m = re.search(r"(encode_kernel|decode_kernel)<(false|true|\d), (\d)((?:, (?:false|true))*)>", name)
     if not m:
         return None
     flags = [f.strip() == "true" for f in m.group(4).split(",")[1:]]
-    # encode_kernel<layout, source, kTab, kLone>, decode_kernel<layout, destination, kLone>
+    # encode_kernel<layout, source, kTab, kSmall>, decode_kernel<layout, destination, kSmall>
     tab = m.group(1) == "encode_kernel" and len(flags) > 0 and flags[0]
-    lone = flags[-1] if (m.group(1) == "encode_kernel" and len(flags) > 1) or (m.group(1) == "decode_kernel" and flags) else False
-    name = m.group(1) + ("_tables" if tab else "") + ("_lone" if lone else "")
+    small = flags[-1] if (m.group(1) == "encode_kernel" and len(flags) > 1) or (m.group(1) == "decode_kernel" and flags) else False
+    name = m.group(1) + ("_tables" if tab else "") + ("_small" if small else "")
     return (name, m.group(2) in ("false", "0"), int(m.group(3)))
 
 
