@@ -1658,15 +1658,22 @@ __global__ __launch_bounds__(64 * HC_WAVES) __attribute__((amdgpu_waves_per_eu(k
                     const uint32_t ssv = (uint32_t)(size_t)(const lds_u8 *)sb + (g < kSK ? g : 0u);
                     const uint32_t sscb = lds_off(&fgk.T.scratch[0]) + 4 * ln;
                     const uint32_t mkb = lds_off(&fgk.T.smark[0]);
+                    // the cached path of the step's symbols: symbol byte -> where[] -> row (level
+                    // 4 too, for the depth test). (Measured: read one step ahead, for the step
+                    // that follows if this one takes all its symbols -- rows and where[] change
+                    // only on the alone path -- grad encode 1.28 -> 1.33 ms.)
+                    auto row_read = [&](uint32_t t0, uint32_t &p4v) __attribute__((always_inline)) {
+                        const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(ssv + t0));
+                        const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
+                        const uint32_t ra = srow + 32 * (wh >> 10);
+                        p4v = opaque(*(const lds_u16 *)(size_t)(ra + 8));  // lane l = 0: level 4
+                        return opaque(*(const lds_u16 *)(size_t)ra);
+                    };
                     do {
                         if (sink.n > 64 - kSK) sink.pack();
                         HC_CNT(1);
                         jmax = min(kSK, ns - t);
-                        const uint32_t sv = opaque(*(const lds_u8 *)(size_t)(ssv + t));
-                        const uint32_t wh = opaque(*(const lds_u16 *)(size_t)(whb + 2 * sv));
-                        const uint32_t ra = srow + 32 * (wh >> 10);
-                        uint32_t pos = opaque(*(const lds_u16 *)(size_t)ra);
-                        const uint32_t p4 = opaque(*(const lds_u16 *)(size_t)(ra + 8));  // lane l = 0: level 4
+                        uint32_t p4, pos = row_read(t, p4);
                         pos = sel(~0ull << (kSK * kSG), kRoot, pos);
                         const uint32_t wa = wtb + 4 * pos;
                         const uint64_t gm = below_mask(kSG * jmax);
