@@ -209,6 +209,10 @@ constexpr uint32_t kRow = 16;       // u16 per cache entry
 // decode -5.5 % / ±0 / +2 %: the retest's ~35-55 instructions cost what the restarts they save do;
 // the decoder's alone, in the blocks of streams that have seen <= 16 symbols (a second copy of the
 // block loop): grad decode -2.7 %, C5 decode +0.3 %, C3 decode +0.8 %)
+// the encoder vote's spread sample: eight segments' loads in flight at once (enc_mode_kernel)
+#ifndef HC_VOTE_BATCH
+#define HC_VOTE_BATCH 1
+#endif
 #ifndef HC_BATCH_RETRY
 #define HC_BATCH_RETRY 0
 #endif
@@ -1315,7 +1319,57 @@ __global__ __launch_bounds__(256) void enc_mode_kernel(Batch bt, uint32_t low_oc
     const bool spread = n > 16384;
     const uint32_t nseg = spread ? 64u : (uint32_t)((n + 255) / 256);
     uint32_t prev_raw = 0, prev_sym = 0, total = 0;  // lane 63's dwords of the last segment; run starts
+#if HC_VOTE_BATCH
+    // the spread segments are independent (each one's first symbol starts a run, its previous raw
+    // byte is the byte before it): kVB segments' loads go out together, then their histogram
+    // updates (one at a time, each waiting for its load, the vote was 64 global round trips long:
+    // 0.11 ms of grad's 1.25 ms encode)
+    if (spread) {
+        constexpr uint32_t kVB = 8;
+        // segment k starts at ((n - 256) k / 63) & ~3, stepped without a 64-bit division per
+        // segment (the scalar unit has none: each was a long SALU sequence, 70 SALU a segment)
+        const uint64_t q = uni64((n - 256) / 63);
+        const uint32_t r = uni((uint32_t)((n - 256) - 63 * q));
+        uint64_t ob = 0;   // q k + (r k) / 63
+        uint32_t oa = 0;   // (r k) % 63
+        for (uint32_t k0 = 0; k0 < 64; k0 += kVB) {
+            uint32_t w[kVB], pr[kVB];
+#pragma unroll
+            for (uint32_t u = 0; u < kVB; ++u) {
+                const uint64_t o = ob & ~3ull;
+                ob += q;
+                oa += r;
+                if (oa >= 63) {
+                    oa -= 63;
+                    ++ob;
+                }
+                w[u] = buf_load(make_rsrc(in + o, 256u), 4 * lane);
+                // the dword ending at the segment's first byte (its top byte: the byte before)
+                // (no branch: a load under one would be waited for at the join)
+                pr[u] = buf_load(make_rsrc(in + (o ? o - 4 : 0), 4u), 0u) & (o ? 0xFF000000u : 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kVB; ++u) {
+                uint32_t sy = w[u];
+                if (kSrc == SRC_RAW_DIFF) {  // transform.cpp:220-229 (m[-1] = 0), bytewise
+                    const uint32_t xp = (w[u] << 8) | (wave_shr1(w[u], pr[u]) >> 24);
+                    sy = ((w[u] | 0x80808080u) - (xp & 0x7F7F7F7Fu)) ^ ((w[u] ^ ~xp) & 0x80808080u);
+                }
+                const uint32_t sp = (sy << 8) | (wave_shr1(sy, 0u) >> 24);
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t i = 4 * lane + j, v = byte_of(sy, j);
+                    const bool start = i == 0 || v != byte_of(sp, j);
+                    if (start) atomicAdd(&h[v], 1u);
+                    total += (uint32_t)__builtin_popcountll(ballot(start));
+                }
+            }
+        }
+    }
+    for (uint32_t k = 0; k < (spread ? 0u : nseg); ++k) {
+#else
     for (uint32_t k = 0; k < nseg; ++k) {
+#endif
         const uint64_t o = spread ? ((n - 256) * k / 63) & ~3ull : 256ull * k;
         const uint32_t len = (uint32_t)min(n - o, (uint64_t)256);
         const uint32_t w = buf_load(make_rsrc(in + o, (len + 3u) & ~3u), 4 * lane);
